@@ -1,0 +1,179 @@
+/*
+ * lbm_hip.h -- C ABI of the MI355X-native D2Q9-BGK engine (liblbm_hip.so).
+ *
+ * This is the drop-in boundary that replaces the Poplar Engine the reference
+ * host (thorbenlouw/lbm-graphcore main/LbmRunner.cpp) drives.  Plain C types
+ * only; no C++ exception crosses it; every call is blocking and non-reentrant
+ * per handle.  The caller owns every host buffer; the library owns all device
+ * memory, streams, events and the RCCL communicator and keeps no caller
+ * pointer after a call returns.
+ *
+ * Layout at the boundary (unchanged from the reference):
+ *   cells      AoS float[ny][nx][9], speed order 0 M,1 E,2 N,3 W,4 S,5 NE,6 NW,7 SW,8 SE
+ *              (main/include/LatticeBoltzmannUtils.hpp:20-22, :125-157)
+ *   obstacles  uint8[ny][nx], row-major, nonzero = blocked
+ *              (main/include/LbmParams.hpp:67-128 stores bool[ny*nx])
+ *   av_vels    float[max_iters]  (LbmRunner.cpp:70, stream "<<av_vel")
+ * Inside the library the lattice is SoA f[9][ny+2][pitch] with a one-cell
+ * ghost ring; the transpose happens in lbm_load_cells / lbm_store, off the
+ * timed path.
+ *
+ * Return codes: 0 on success, a negative LBM_E* value on failure; the message
+ * is available from lbm_last_error().
+ */
+#ifndef LBM_HIP_H
+#define LBM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBM_ABI_VERSION 1
+
+enum {
+    LBM_OK = 0,
+    LBM_E_INVALID = -1,     /* bad argument / unsupported configuration */
+    LBM_E_HIP = -2,         /* HIP runtime error */
+    LBM_E_RCCL = -3,        /* RCCL error */
+    LBM_E_NOMEM = -4,       /* host or device allocation failed */
+    LBM_E_STATE = -5,       /* call out of order (e.g. lbm_run before lbm_load_cells) */
+    LBM_E_INTERNAL = -6
+};
+
+/* lbm::Params (main/include/LbmParams.hpp:16-65): the 7-line params file. */
+typedef struct lbm_params {
+    int32_t nx;            /* cells in x (columns) */
+    int32_t ny;            /* cells in y (rows) */
+    int32_t max_iters;     /* steps per lbm_run */
+    int32_t reynolds_dim;
+    float density;
+    float accel;
+    float omega;
+} lbm_params;
+
+enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
+enum { LBM_KERNEL_AUTO = 0, LBM_KERNEL_SCALAR = 1, LBM_KERNEL_VEC4 = 2 };
+
+/*
+ * Placement of the 2-D block decomposition.
+ *   LOCAL: this process owns every sub-domain; sub-domain i lives on device
+ *          devices[i % num_devices] (NULL -> device i % visible devices) and
+ *          halos move by device copies (peer copies across devices).  With
+ *          several sub-domains on one device this is the loop-back mode the
+ *          tests use to exercise the multi-GPU path on one GPU.
+ *   RCCL:  one process per GPU; this process owns sub-domain `rank` on
+ *          devices[0] (or `rank` % visible devices) and halos move with
+ *          grouped ncclSend/ncclRecv over xGMI.  rccl_unique_id must hold the
+ *          128 bytes from lbm_rccl_unique_id() of rank 0.
+ * grid_rows/grid_cols = 0 selects the reference's partitionForIpus rule
+ * (main/include/StructuredGridUtils.hpp:472-561) for `parts` sub-domains.
+ */
+typedef struct lbm_config {
+    int32_t parts;          /* number of sub-domains (>= 1) */
+    int32_t grid_rows;      /* 0 = choose by rule */
+    int32_t grid_cols;      /* 0 = choose by rule */
+    int32_t transport;      /* LBM_TRANSPORT_* */
+    int32_t rank;           /* RCCL only */
+    int32_t world;          /* RCCL only; must equal parts */
+    const int32_t *devices; /* optional device list */
+    int32_t num_devices;
+    const uint8_t *rccl_unique_id; /* 128 bytes, RCCL only */
+    int32_t kernel;         /* LBM_KERNEL_* */
+    int32_t graph_steps;    /* >0: replay the step loop as hipGraphs of this many steps (single sub-domain) */
+} lbm_config;
+
+typedef struct lbm_handle lbm_handle;
+
+/* Sub-domain rectangle in global cell coordinates. */
+typedef struct lbm_rect {
+    int32_t x0, y0, w, h;
+} lbm_rect;
+
+/* ---- host-only helpers (no GPU needed) -------------------------------- */
+
+int32_t lbm_abi_version(void);
+
+/*
+ * Reference partition rule, StructuredGridUtils.hpp:472-561 partitionForIpus:
+ * parts in {1,2,4,8,16} -> rows x cols (2: by imbalance, 8: 4x2 or 2x4 by
+ * imbalance), round-robin row/col allocation (:161-165), rank = row*cols+col
+ * (:548).  Writes rows/cols and, if rects != NULL, `parts` rectangles.
+ */
+int lbm_partition(int32_t nx, int32_t ny, int32_t parts, int32_t grid_rows, int32_t grid_cols,
+                  int32_t *rows_out, int32_t *cols_out, lbm_rect *rects);
+
+/* Number of visible HIP devices (0 on a host without GPUs; never fails). */
+int32_t lbm_device_count(void);
+
+/* 128-byte RCCL unique id for rank 0 to broadcast (ncclGetUniqueId). */
+int lbm_rccl_unique_id(uint8_t out[128]);
+
+/* ---- engine ------------------------------------------------------------ */
+
+/*
+ * ≙ Engine(Executable::deserialize(..)) + connectStream(">>obstacles") +
+ *   engine.load(device)  (main/LbmRunner.cpp:81-96).
+ * Single process driving `num_gpus` devices (LbmRunner's -n), LOCAL transport.
+ * obstacles: uint8[ny][nx] (full domain).
+ */
+int lbm_create(const lbm_params *params, const uint8_t *obstacles, int32_t num_gpus,
+               lbm_handle **out);
+
+/* As lbm_create with an explicit placement (see lbm_config). */
+int lbm_create_ex(const lbm_params *params, const uint8_t *obstacles, const lbm_config *config,
+                  lbm_handle **out);
+
+/*
+ * ≙ engine.run(0) with stream ">>cells" (LbmRunner.cpp:86-100):
+ * host AoS float[ny][nx][9] (full domain) -> device.  Every process passes
+ * the full-domain array; each takes its sub-domain(s).
+ */
+int lbm_load_cells(lbm_handle *h, const float *cells_aos);
+
+/* Equilibrium initial state on the device (≙ lbm::Cells::initialise,
+ * LatticeBoltzmannUtils.hpp:137-157, without a host array). */
+int lbm_init_equilibrium(lbm_handle *h);
+
+/*
+ * ≙ engine.run(1) (LbmRunner.cpp:102-104; graph program LbmAoS.cpp:349-356):
+ * the one-time conditional accelerate of row ny-2, then max_iters fused
+ * steps, with av_vels kept on the device.  Blocking.
+ */
+int lbm_run(lbm_handle *h);
+
+/* `steps` fused steps, optionally preceded by the first accelerate (bench / tests). */
+int lbm_run_steps(lbm_handle *h, int32_t steps, int32_t accelerate_first);
+
+/*
+ * ≙ engine.run(2) with "<<cells"/"<<av_vel" (LbmRunner.cpp:85-108).
+ * cells_aos: full-domain AoS (may be NULL).  In RCCL mode only this rank's
+ * sub-domain is written into the full-size array (others untouched).
+ * av_vels: float[n_av] for the last lbm_run/lbm_run_steps, each entry
+ * sum over ALL ranks of |u| / total free cells (may be NULL).
+ */
+int lbm_store(lbm_handle *h, float *cells_aos, float *av_vels, int32_t n_av);
+
+/* ≙ engine.readTensor("readTimer") (LbmRunner.cpp:133-144):
+ * device-event seconds of the last lbm_run / lbm_run_steps. */
+int lbm_last_run_seconds(lbm_handle *h, double *seconds);
+
+/* Total non-obstacle cells of the full domain (LastChance.cpp:486-493). */
+int64_t lbm_total_free_cells(lbm_handle *h);
+
+/* Local sub-domain rectangles of this handle (LOCAL: all; RCCL: this rank's). */
+int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *n_out);
+
+/* Which step kernel the handle uses (LBM_KERNEL_SCALAR or LBM_KERNEL_VEC4). */
+int32_t lbm_kernel_in_use(lbm_handle *h);
+
+const char *lbm_last_error(lbm_handle *h);
+
+void lbm_destroy(lbm_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LBM_HIP_H */
