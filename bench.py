@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""Benchmark of the D2Q9-BGK hot path (BASELINE.json metric: MLUPS, fp32).
+
+  python bench.py [--gpus N --steps K --warmup W] [--tile 8192x8192] [--kernel auto|scalar|vec4]
+
+One "step" = one fused lattice update of every cell (pull-stream, rebound /
+BGK collision, folded acceleration, |u| reduction, halo exchange).
+
+Workload (config.workload): BASELINE config 3, 8192x8192 fp32 cells per GPU
+with deterministic synthetic obstacles (walls on the four borders plus one
+full interior column at x = nx/3, mimicking obstacles_1024x1024.dat), rho 0.1,
+accel 0.005, omega 1.85, equilibrium start.  For N > 1 the per-GPU tile is
+fixed (weak scaling): the global grid is (8192*R) x (8192*C) with R x C =
+1x2, 2x2, 2x4 from the reference's partitionForIpus rule, one process per
+GPU, halos over RCCL.  Rank 0 at N=1 also runs BASELINE config 2 (the
+reference 1024x1024 problem, 20 000 steps) and the CPU baseline.
+
+Timed region: K steps between barrier + torch.cuda.synchronize() pairs, max
+over ranks.  value = all cells x K / seconds / 1e6 (whole job).
+
+roofline: 72 algorithmic bytes per cell update (9 fp32 loads + 9 fp32
+stores; the 1-byte obstacle mask is excluded), per launch = 72 x cells of
+the launch, divided by the average step-kernel duration measured with HIP
+events recorded by the library on the kernel's own stream over the timed
+region; peak = 8000 GB/s (MI355X HBM3E spec).  traffic = PMC-measured HBM
+bytes per launch from profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950
+correction) when a profile of this workload exists, else null.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "lbm-graphcore_amd"
+for _p in (str(ROOT), str(PKG)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from lbm_amd import io as lio  # noqa: E402
+from lbm_amd import native  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+BYTES_PER_UPDATE = 72
+METRIC = "MLUPS at 1024² and 8192² fp32, 1/2/4/8 MI355X; % HBM roofline"
+
+
+def synthetic_obstacles(nx: int, ny: int) -> np.ndarray:
+    o = np.zeros((ny, nx), np.uint8)
+    o[0, :] = 1
+    o[-1, :] = 1
+    o[:, 0] = 1
+    o[:, -1] = 1
+    o[:, nx // 3] = 1
+    return o
+
+
+def weak_grid(n: int):
+    return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}[n]
+
+
+def log(msg: str) -> None:
+    print(msg, file=sys.stderr, flush=True)
+
+
+def load_traffic(workload_key: str):
+    """Per-launch HBM bytes from the committed PMC profile of this workload, if any."""
+    f = ROOT / "profiles" / "traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except (ValueError, OSError):
+        return None
+
+
+def cpu_baseline() -> dict | None:
+    """The reference's own LastChance (oracle/_ref) on a bounded sample of the
+    1024x1024 reference problem, single thread on this host."""
+    from oracle import oracle  # checker / baseline only
+    iters = 500
+    gold = ROOT / "tests" / "golden" / "params"
+    with tempfile.TemporaryDirectory() as wd:
+        pf = Path(wd) / "bench.params"
+        pf.write_text(f"1024\n1024\n{iters}\n10\n0.1\n0.01\n1.85\n")
+        of = gold / "obstacles_1024x1024.dat"
+        if oracle.REF_LASTCHANCE.exists():
+            try:
+                r = oracle.run_reference(str(pf), str(of), wd)
+                secs = r["elapsed_s"]
+                return {"value": round(1024 * 1024 * iters / secs / 1e6, 2), "unit": "MLUPS", "cores": 1,
+                        "kind": "reference",
+                        "sample": f"main/LastChance.cpp (compiled -O3 -ffp-contract=off) on the 1024x1024 "
+                                  f"reference problem, first {iters} of 20000 steps, {secs:.2f} s, 1 thread"}
+            except Exception as exc:  # fall back to the restatement
+                log(f"reference CPU baseline failed: {exc}")
+        p = lio.Params.from_file(str(pf))
+        obst = lio.read_obstacles(p.nx, p.ny, str(of))
+        t = time.perf_counter()
+        oracle.run(p, obst)
+        secs = time.perf_counter() - t
+        return {"value": round(1024 * 1024 * iters / secs / 1e6, 2), "unit": "MLUPS", "cores": 1, "kind": "port",
+                "sample": f"oracle/lbm_oracle.c restatement, 1024x1024 reference problem, {iters} steps, "
+                          f"{secs:.2f} s, 1 thread"}
+
+
+def aux_1024(kernel: int) -> dict:
+    """BASELINE config 2: the reference 1024x1024 problem, all 20 000 steps, 1 GPU."""
+    gold = ROOT / "tests" / "golden" / "params"
+    p = lio.Params.from_file(str(gold / "input_1024x1024.params"))
+    obst = lio.read_obstacles(p.nx, p.ny, str(gold / "obstacles_1024x1024.dat"))
+    with native.Engine(p, obst, devices=[0], kernel=kernel) as e:
+        e.load_cells(lio.init_cells(p))
+        e.run()                      # first run: warm-up + results
+        _, av = e.store()
+        e.run()                      # timed re-run (device events), as LbmRunner's readTimer runs
+        secs = e.last_run_seconds()
+    cells = p.nx * p.ny
+    return {"grid": "1024x1024", "steps": p.max_iters, "mlups": round(cells * p.max_iters / secs / 1e6, 1),
+            "ms_per_step": round(secs / p.max_iters * 1e3, 5),
+            "reynolds": lio.reynolds_number(p, float(av[-1])),
+            "note": "lattice pair (151 MB) fits the 256 MB Infinity Cache: not an HBM-roofline number"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--tile", default="8192x8192", help="cells per GPU, NXxNY")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "scalar", "vec4"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-aux", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    n = world
+    kernel = {"auto": native.KERNEL_AUTO, "scalar": native.KERNEL_SCALAR, "vec4": native.KERNEL_VEC4}[args.kernel]
+
+    import torch
+    import torch.distributed as dist
+    dist_on = world > 1
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+
+    tnx, tny = (int(v) for v in args.tile.lower().split("x"))
+    R, C = weak_grid(n)
+    nx, ny = tnx * C, tny * R
+    p = lio.Params(nx, ny, args.steps, 10, 0.1, 0.005, 1.85)
+    obst = synthetic_obstacles(nx, ny)
+
+    uid = None
+    if dist_on:
+        box = [native.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    eng = native.Engine(p, obst, parts=n, grid=(R, C),
+                        transport=native.TRANSPORT_RCCL if dist_on else native.TRANSPORT_LOCAL,
+                        rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel)
+    eng.init_equilibrium()
+    if args.warmup > 0:
+        eng.run_steps(args.warmup, accelerate_first=True)
+
+    def barrier():
+        if dist_on:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run_steps(args.steps, accelerate_first=False)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    dev_secs = eng.last_run_seconds()
+    if dist_on:
+        t = torch.tensor([elapsed, dev_secs], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, dev_secs = float(t[0]), float(t[1])
+    _, av = eng.store(cells=False, n_av=args.steps)
+    finite = bool(np.all(np.isfinite(av)))
+    kernel_used = eng.kernel_in_use()
+    eng.close()
+
+    total_cells = nx * ny
+    value = total_cells * args.steps / elapsed / 1e6
+    per_launch_s = dev_secs / args.steps
+    cells_per_gpu = tnx * tny
+    achieved = BYTES_PER_UPDATE * cells_per_gpu / per_launch_s / 1e9
+    wl_key = f"{tnx}x{tny}"
+    traffic = load_traffic(wl_key)
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "MLUPS",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (deterministic obstacles: border walls + interior column at x=nx/3; equilibrium start)",
+        "config": {"workload": f"D2Q9-BGK fused step, {tnx}x{tny} fp32 cells per GPU",
+                   "global_grid": f"{nx}x{ny}", "decomposition": f"{R}x{C}",
+                   "parallelism": "2-D block decomposition, RCCL halo exchange" if n > 1 else "single GPU",
+                   "kernel": kernel_used},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_launch": BYTES_PER_UPDATE * cells_per_gpu,
+                     "avg_launch_ms": round(per_launch_s * 1e3, 5)},
+        "av_vels_finite": finite,
+    }
+    if rank == 0 and n == 1:
+        if not args.no_aux:
+            try:
+                out["aux"] = {"config2_1024x1024": aux_1024(kernel)}
+            except Exception as exc:
+                out["aux"] = {"config2_1024x1024": {"error": str(exc)}}
+        if not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline()
+            except Exception as exc:
+                out["cpu_baseline"] = None
+                log(f"cpu baseline failed: {exc}")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -104,6 +104,17 @@ int32_t lbm_abi_version(void);
 int lbm_partition(int32_t nx, int32_t ny, int32_t parts, int32_t grid_rows, int32_t grid_cols,
                   int32_t *rows_out, int32_t *cols_out, lbm_rect *rects);
 
+/*
+ * Halo exchange plan (host-only): for each of the 8 directions d (order E, N,
+ * W, S, NE, NW, SW, SE = velocities of speeds 1..8) writes 6 ints
+ * {dx, dy, nplanes, plane0, plane1, plane2} (unused planes = -1): the
+ * populations that leave a sub-domain through side d and land in the
+ * neighbour's ghost ring on the opposite side.  Replaces the stitched-halo
+ * views of the reference (GraphcoreUtils.hpp:119-127,
+ * StructuredGridUtils.hpp:805-851), which copy whole 9-speed cells.
+ */
+int lbm_halo_plan(int32_t table[48]);
+
 /* Number of visible HIP devices (0 on a host without GPUs; never fails). */
 int32_t lbm_device_count(void);
 

@@ -65,9 +65,9 @@ struct StepArgs {
     int accel_row;          // local row carrying the folded acceleration, -1 if none
     float omega, omo, w1, w2;
     int nrect;
-    int total;              // total work items over all rects
+    int total;              // total tiles (BLOCK work items each) over all rects
     Rect rect[MAX_RECTS];
-    int rect_begin[MAX_RECTS];  // first work item of each rect (INT_MAX when unused)
+    int rect_begin[MAX_RECTS];  // first tile of each rect (INT_MAX when unused); a tile never spans rects
     EdgeDst dst[8];
     // average-velocity reduction
     float *partials_out;        // this launch writes partials_out[blockIdx.x]

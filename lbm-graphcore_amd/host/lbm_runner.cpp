@@ -1,0 +1,177 @@
+// lbm_runner -- the reference's LbmRunner CLI (main/LbmRunner.cpp:11-147) on
+// top of the HIP engine's C ABI instead of a Poplar Engine.
+//
+//   lbm_runner --params P --obstacles O [-n N] [--device gpu|loopback] [-d] [--exe ignored]
+//              [--runs 5] [--kernel auto|scalar|vec4] [--out-dir DIR]
+//
+// Flow (same program numbering as the reference):
+//   load params/obstacles -> initialise cells on host -> create engine
+//   run(0) ≙ lbm_load_cells -> run(1) ≙ lbm_run (accelerate + maxIters steps)
+//   run(2) ≙ lbm_store -> write av_vels.dat / final_state.dat
+//   print ==done==, compute time, Reynolds number (av_vels[maxIters-1])
+//   then `runs` more lbm_run calls timed by device events (≙ readTimer).
+// --device loopback places all N sub-domains on GPU 0 (the emulator analogue
+// of --device ipumodel: exercises the multi-GPU halo path on one device).
+#include <cstdlib>
+#include <cstring>
+#include <iomanip>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "lbm_host.hpp"
+
+namespace {
+
+void usage(const char *exe) {
+    std::cerr << exe << " - Runs the Lattice Boltzmann D2Q9-BGK engine on MI355X GPUs\n"
+              << "Usage:\n  " << exe << " [OPTION...]\n\n"
+              << "  -d, --debug          Print per-phase detail\n"
+              << "      --device arg     gpu or loopback (default: gpu)\n"
+              << "  -n, --num-gpus arg   number of GPUs / sub-domains to use (default: 1)\n"
+              << "      --exe arg        accepted for compatibility with the reference (ignored)\n"
+              << "      --params arg     filename of parameters file\n"
+              << "      --obstacles arg  filename of obstacles file\n"
+              << "      --runs arg       timed re-runs after the first (default: 5)\n"
+              << "      --kernel arg     auto, scalar or vec4 (default: auto)\n"
+              << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n";
+}
+
+}  // namespace
+
+int main(int argc, char *argv[]) {
+    std::string paramsFile, obstaclesFile, device = "gpu", exeFile, kernel = "auto", outDir = ".";
+    int numGpus = 1, runs = 5;
+    bool debug = false;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        std::string val;
+        const auto eq = a.find('=');
+        if (a.rfind("--", 0) == 0 && eq != std::string::npos) {
+            val = a.substr(eq + 1);
+            a = a.substr(0, eq);
+        }
+        auto next = [&](std::string &dst) -> bool {
+            if (!val.empty()) { dst = val; return true; }
+            if (i + 1 >= argc) return false;
+            dst = argv[++i];
+            return true;
+        };
+        std::string v;
+        if (a == "-d" || a == "--debug") {
+            debug = true;
+        } else if (a == "--device") {
+            if (!next(device)) { usage(argv[0]); return EXIT_FAILURE; }
+        } else if (a == "-n" || a == "--num-gpus" || a == "--num-ipus") {
+            if (!next(v)) { usage(argv[0]); return EXIT_FAILURE; }
+            numGpus = std::atoi(v.c_str());
+        } else if (a == "--exe") {
+            if (!next(exeFile)) { usage(argv[0]); return EXIT_FAILURE; }
+        } else if (a == "--params") {
+            if (!next(paramsFile)) { usage(argv[0]); return EXIT_FAILURE; }
+        } else if (a == "--obstacles") {
+            if (!next(obstaclesFile)) { usage(argv[0]); return EXIT_FAILURE; }
+        } else if (a == "--runs") {
+            if (!next(v)) { usage(argv[0]); return EXIT_FAILURE; }
+            runs = std::atoi(v.c_str());
+        } else if (a == "--kernel") {
+            if (!next(kernel)) { usage(argv[0]); return EXIT_FAILURE; }
+        } else if (a == "--out-dir") {
+            if (!next(outDir)) { usage(argv[0]); return EXIT_FAILURE; }
+        } else if (a == "-h" || a == "--help") {
+            usage(argv[0]);
+            return EXIT_SUCCESS;
+        } else {
+            usage(argv[0]);
+            return EXIT_FAILURE;
+        }
+    }
+    if (paramsFile.empty() || obstaclesFile.empty() || numGpus < 1 || (device != "gpu" && device != "loopback")) {
+        usage(argv[0]);
+        return EXIT_FAILURE;
+    }
+    if (debug) std::cout << "Capturing profile information during this run." << std::endl;
+
+    auto params = lbmhost::Params::fromFile(paramsFile);
+    if (!params.has_value()) {
+        std::cerr << "Could not parse parameters file. Aborting" << std::endl;
+        return EXIT_FAILURE;
+    }
+    auto obstacles = lbmhost::Obstacles::fromFile(params->nx, params->ny, obstaclesFile);
+    if (!obstacles.has_value()) {
+        std::cerr << "Could not parse obstacles file" << std::endl;
+        return EXIT_FAILURE;
+    }
+    const int ndev = lbm_device_count();
+    if (ndev <= 0) {
+        std::cerr << "No HIP device visible" << std::endl;
+        return EXIT_FAILURE;
+    }
+    if (device == "gpu")
+        std::cout << "Running on " << numGpus << " GPU(s)" << std::endl;
+    else
+        std::cout << "Running " << numGpus << " sub-domain(s) in loop-back on GPU 0" << std::endl;
+
+    double total_compute_time = 0.0;
+    auto cells = lbmhost::initialiseCells(*params);
+    std::vector<float> av_vels(params->maxIters, 0.0f);
+
+    lbm_handle *h = nullptr;
+    const lbm_params abi = params->abi();
+    std::vector<int32_t> devs;
+    if (device == "loopback") devs.push_back(0);
+    lbmhost::timedStep("Creating engine and loading obstacles", [&]() {
+        lbm_config cfg{};
+        cfg.parts = numGpus;
+        cfg.transport = LBM_TRANSPORT_LOCAL;
+        cfg.devices = devs.empty() ? nullptr : devs.data();
+        cfg.num_devices = (int32_t)devs.size();
+        cfg.kernel = kernel == "scalar" ? LBM_KERNEL_SCALAR : (kernel == "vec4" ? LBM_KERNEL_VEC4 : LBM_KERNEL_AUTO);
+        lbmhost::check(lbm_create_ex(&abi, obstacles->data.data(), &cfg, &h), nullptr, "lbm_create_ex");
+    });
+    if (debug) {
+        std::vector<lbm_rect> rects(numGpus);
+        int32_t n = 0;
+        lbm_local_rects(h, rects.data(), numGpus, &n);
+        for (int i = 0; i < n; ++i)
+            std::cout << "sub-domain " << i << ": " << rects[i].w << "x" << rects[i].h << " at (row:" << rects[i].y0
+                      << ",col:" << rects[i].x0 << ")" << std::endl;
+        std::cout << "step kernel: " << (lbm_kernel_in_use(h) == LBM_KERNEL_VEC4 ? "vec4" : "scalar") << std::endl;
+    }
+    lbmhost::timedStep("Running copy to device step", [&]() {
+        lbmhost::check(lbm_load_cells(h, cells.data()), h, "lbm_load_cells");
+    });
+    total_compute_time += lbmhost::timedStep("Running LBM", [&]() { lbmhost::check(lbm_run(h), h, "lbm_run"); });
+    lbmhost::timedStep("Running copy to host step", [&]() {
+        lbmhost::check(lbm_store(h, cells.data(), av_vels.data(), (int32_t)av_vels.size()), h, "lbm_store");
+    });
+    lbmhost::timedStep("Writing output files ", [&]() {
+        lbmhost::writeAverageVelocities(outDir + "/av_vels.dat", av_vels);
+        lbmhost::writeResults(outDir + "/final_state.dat", *params, *obstacles, cells);
+    });
+
+    std::cout << "==done==" << std::endl;
+    std::cout << "Total compute time was \t" << std::right << std::setw(12) << std::setprecision(5)
+              << total_compute_time << "s" << std::endl;
+    const float lastAv = params->maxIters > 0 ? av_vels[params->maxIters - 1] : 0.f;
+    std::cout << "Reynolds number:  \t" << std::right << std::setw(12) << std::setprecision(12) << std::scientific
+              << lbmhost::reynoldsNumber(*params, lastAv) << std::endl;
+
+    if (runs > 0) {
+        std::cout << "Now doing " << runs << " runs and averaging GPU-reported timing:" << std::endl;
+        double secs = 0.0;
+        for (int r = 0; r < runs; ++r) {
+            lbmhost::check(lbm_run(h), h, "lbm_run");
+            double s = 0.0;
+            lbm_last_run_seconds(h, &s);
+            secs += s;
+        }
+        const double avg = secs / runs;
+        const double mlups = (double)params->nx * params->ny * params->maxIters / avg / 1e6;
+        std::cout << "Average GPU timing for program is: " << std::fixed << std::setprecision(5) << std::setw(12)
+                  << avg << "s" << std::endl;
+        std::cout << "MLUPS: " << std::fixed << std::setprecision(1) << mlups << std::endl;
+    }
+    lbm_destroy(h);
+    return EXIT_SUCCESS;
+}

@@ -1,0 +1,214 @@
+"""HIP path parity, through the C ABI (liblbm_hip.so), against the CPU oracle.
+
+Bar: the lattice is BITWISE identical to the oracle (same fp32 expressions,
+no FMA contraction, correctly rounded div/sqrt); av_vels differ only by
+summation order (tree vs sequential), rtol stated per test; the reference
+gate (check.py semantics, 1 %) passes on all four reference grids.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, GRIDS, load_problem, oracle_av_vels, oracle_manifest, small_problems
+from lbm_amd import check as lcheck
+from lbm_amd import io as lio
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+# av_vels: per-step sum of |u| over up to 1M cells in fp32; the oracle adds
+# sequentially, the GPU in fixed-order trees.  Observed differences are far
+# below this; the reference gate is 1e-2.
+AV_RTOL = 2e-4
+
+
+def sha(cells):
+    return hashlib.sha256(np.ascontiguousarray(cells, dtype="<f4").tobytes()).hexdigest()
+
+
+def gpu_run(native, p, obst, cells0, steps, accelerate=True, **kw):
+    with native.Engine(p, obst, **kw) as e:
+        e.load_cells(cells0)
+        e.run_steps(steps, accelerate_first=accelerate)
+        cells, av = e.store(n_av=steps)
+        kernel = e.kernel_in_use()
+    return cells, av, kernel
+
+
+# ---------------------------------------------------------------- KATs ----
+
+def test_accelerate_kat_gpu(gpu_lib):
+    p = lio.Params(3, 2, 0, 10, 9.0, 1.0, 1.85)
+    cells = np.array([[1, 0.5, 1, 1, 1, 1, 1, 1, 1], list(range(9)), list(range(9)),
+                      list(range(2, 11)), list(range(2, 11)), list(range(2, 11))], np.float32).reshape(2, 3, 9)
+    obst = np.array([[0, 1, 0], [0, 1, 1]], np.uint8)
+    out, _, _ = gpu_run(gpu_lib, p, obst, cells, 0, accelerate=True)
+    ref = cells.copy()
+    oracle.accelerate(p, ref, obst)
+    assert np.array_equal(out, ref)
+    assert np.array_equal(out[0, 2], np.array([0, 2, 2, 2, 4, 5.25, 5.75, 6.75, 8.25], np.float32))
+
+
+def test_collision_rebound_kat_gpu(gpu_lib):
+    vals = [2.30, 2.31, 2.32, 2.33, 2.34, 2.35, 2.36, 2.37, 2.38]
+    p = lio.Params(2, 1, 1, 10, 0.1, 0.0, 1.0)
+    cells = np.broadcast_to(np.asarray(vals, np.float32), (1, 2, 9)).copy()
+    obst = np.array([[1, 0]], np.uint8)
+    out, av, _ = gpu_run(gpu_lib, p, obst, cells, 1, accelerate=False)
+    ref, tot = oracle.step(p, cells, obst)
+    assert np.array_equal(out, ref)
+    assert np.array_equal(out[0, 0], np.asarray(vals, np.float32)[[0, 3, 4, 1, 2, 7, 8, 5, 6]])
+    assert av[0] == pytest.approx(tot / 1.0, rel=1e-6)
+
+
+@pytest.mark.parametrize("nx,ny", [(5, 3), (8, 8), (64, 4), (1, 4), (12, 1)])
+def test_periodic_streaming_gpu(gpu_lib, nx, ny):
+    rng = np.random.default_rng(nx * 100 + ny)
+    cells = rng.random((ny, nx, 9), dtype=np.float32) + 0.5
+    p = lio.Params(nx, ny, 1, 10, 0.1, 0.0, 0.0)
+    out, _, _ = gpu_run(gpu_lib, p, np.zeros((ny, nx), np.uint8), cells, 1, accelerate=False)
+    cx = [0, 1, 0, -1, 0, 1, -1, -1, 1]
+    cy = [0, 0, 1, 0, -1, 1, 1, -1, -1]
+    for k in range(9):
+        assert np.array_equal(out[..., k], np.roll(cells[..., k], (cy[k], cx[k]), axis=(0, 1))), k
+
+
+# ------------------------------------------------------ small vectors ----
+
+@pytest.mark.parametrize("kernel", ["scalar", "vec4"])
+def test_small_vectors_bitwise(gpu_lib, kernel):
+    kid = {"scalar": gpu_lib.KERNEL_SCALAR, "vec4": gpu_lib.KERNEL_VEC4}[kernel]
+    ran = 0
+    for name, (p, obst, cells0, after) in small_problems().items():
+        if kernel == "vec4" and p.nx % 4:
+            continue
+        for n, (ref_cells, ref_av) in after.items():
+            cells, av, used = gpu_run(gpu_lib, p, obst, cells0, n, kernel=kid)
+            assert used == kernel
+            assert np.array_equal(cells, ref_cells), (name, n, kernel)
+            np.testing.assert_allclose(av, ref_av, rtol=1e-5, err_msg=f"{name} {n}")
+            ran += 1
+    assert ran > 0
+
+
+@pytest.mark.parametrize("parts,grid", [(2, (1, 2)), (2, (2, 1)), (4, (2, 2)), (8, (2, 4)), (8, (4, 2)), (3, (3, 1)),
+                                        (6, (3, 2))])
+@pytest.mark.parametrize("kernel", ["scalar", "vec4"])
+def test_decomposed_loopback_bitwise(gpu_lib, parts, grid, kernel):
+    """N sub-domains on GPU 0 (device-copy halos): lattice bitwise == single domain."""
+    p, obst = load_problem("128x256", iters=23)
+    kid = {"scalar": gpu_lib.KERNEL_SCALAR, "vec4": gpu_lib.KERNEL_VEC4}[kernel]
+    cells0 = lio.init_cells(p)
+    ref, ref_av = oracle.run(p, obst, 23, cells0)
+    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 23, parts=parts, grid=grid, devices=[0], kernel=kid)
+    assert used == kernel
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.parametrize("parts", [2, 4, 8, 16])
+def test_decomposed_small_ragged(gpu_lib, parts):
+    """Ragged sub-domains (round-robin split, widths not multiples of 4) use the scalar kernel."""
+    p = lio.Params(37, 29, 7, 10, 0.1, 0.02, 1.7)
+    obst = np.zeros((29, 37), np.uint8)
+    obst[0, :] = obst[-1, :] = 1
+    obst[5:20, 11] = 1
+    rng = np.random.default_rng(parts)
+    cells0 = (lio.init_cells(p) * (1 + 0.02 * rng.standard_normal((29, 37, 9)))).astype(np.float32)
+    ref, ref_av = oracle.run(p, obst, 7, cells0)
+    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 7, parts=parts, devices=[0])
+    assert used == "scalar"
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+# ------------------------------------------------ reference grids ----
+
+@pytest.mark.parametrize("grid", GRIDS)
+def test_reference_grid_full_run(gpu_lib, grid, tmp_path):
+    """Full maxIters run: final lattice bitwise == oracle (sha256), av_vels ~ oracle,
+    and the reference gate (check.py, 1 %) against check/*.dat passes."""
+    p, obst = load_problem(grid)
+    m = oracle_manifest(grid)
+    with gpu_lib.Engine(p, obst) as e:
+        e.load_cells(lio.init_cells(p))
+        e.run()
+        cells, av = e.store()
+        assert e.total_free_cells() == m["free_cells"]
+    assert sha(cells) == m["final_f_sha256"]
+    np.testing.assert_allclose(av, oracle_av_vels(grid), rtol=AV_RTOL)
+    assert lio.reynolds_number(p, float(av[-1])) == pytest.approx(m["reynolds_last_av"], rel=AV_RTOL)
+    lio.write_average_velocities(str(tmp_path / "av_vels.dat"), av)
+    ref_av = lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz")
+    assert abs(lcheck.diff_values(ref_av, lcheck.load_av_vels(tmp_path / "av_vels.dat"))["max_diff_pcnt"]) < 1.0
+    fs_fixture = GOLD / "check" / f"{grid}.final_state.dat.gz"
+    if fs_fixture.exists():
+        lio.write_results(str(tmp_path / "final_state.dat"), p, obst, cells)
+        res = lcheck.compare(GOLD / "check" / f"{grid}.av_vels.dat.gz", fs_fixture, tmp_path / "av_vels.dat",
+                             tmp_path / "final_state.dat", 1.0)
+        assert res["passed"], res
+
+
+def test_determinism_and_rerun(gpu_lib):
+    """Two runs give bitwise-identical lattices and av_vels; lbm_run continues from the
+    current state like the reference's repeated engine.run(1)."""
+    p, obst = load_problem("128x128", iters=300)
+    outs = []
+    for _ in range(2):
+        with gpu_lib.Engine(p, obst) as e:
+            e.load_cells(lio.init_cells(p))
+            e.run()
+            e.run()
+            outs.append(e.store())
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    cells = lio.init_cells(p)
+    c1, _ = oracle.run(p, obst, 300, cells)
+    c2, av2 = oracle.run(p, obst, 300, c1)
+    assert np.array_equal(outs[0][0], c2)
+    np.testing.assert_allclose(outs[0][1], av2, rtol=1e-4)
+
+
+def test_large_grid_steps_and_conservation(gpu_lib):
+    """8192^2 (the roofline config): 2 steps bitwise vs oracle, then mass conserved over 200 steps."""
+    n = 8192
+    p = lio.Params(n, n, 2, 10, 0.1, 0.005, 1.85)
+    obst = np.zeros((n, n), np.uint8)
+    obst[0, :] = obst[-1, :] = 1
+    obst[:, 0] = obst[:, -1] = 1
+    obst[:, n // 3] = 1
+    cells0 = lio.init_cells(p)
+    ref, ref_av = oracle.run(p, obst, 2, cells0)
+    with gpu_lib.Engine(p, obst) as e:
+        assert e.kernel_in_use() == "vec4"
+        e.init_equilibrium()
+        e.run_steps(2, accelerate_first=True)
+        cells, av = e.store(n_av=2)
+        assert np.array_equal(cells, ref)
+        np.testing.assert_allclose(av, ref_av, rtol=AV_RTOL)
+        m0 = np.sum(cells, dtype=np.float64)
+        e.run_steps(200)
+        cells2, av2 = e.store(n_av=200)
+    assert np.sum(cells2, dtype=np.float64) == pytest.approx(m0, rel=1e-5)
+    assert np.all(np.isfinite(av2)) and av2[-1] > av2[0]
+
+
+# ------------------------------------------------------------ errors ----
+
+def test_abi_errors(gpu_lib):
+    p = lio.Params(16, 8, 4, 10, 0.1, 0.005, 1.85)
+    obst = np.zeros((8, 16), np.uint8)
+    e = gpu_lib.Engine(p, obst)
+    with pytest.raises(gpu_lib.LbmError) as ei:
+        e.run()
+    assert ei.value.code == gpu_lib.LBM_E_STATE
+    e.close()
+    with pytest.raises(gpu_lib.LbmError) as ei:
+        gpu_lib.Engine(lio.Params(13, 8, 4, 10, 0.1, 0.005, 1.85), np.zeros((8, 13), np.uint8),
+                       kernel=gpu_lib.KERNEL_VEC4)
+    assert ei.value.code == gpu_lib.LBM_E_INVALID
+    with pytest.raises(gpu_lib.LbmError) as ei:
+        gpu_lib.Engine(p, obst, parts=3)  # no partitionForIpus rule for 3 without an explicit grid
+    assert ei.value.code == gpu_lib.LBM_E_INVALID
