@@ -36,11 +36,13 @@
 #include "lbm_layout.hpp"
 
 namespace lbm {
-hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hipStream_t s);
+hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, int flags, int min_waves,
+                       hipStream_t s);
 hipError_t launch_finalize(const float *partials, int n, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
-hipError_t launch_init_equilibrium(float *f, long long P, float c0, float c1, float c2, hipStream_t s);
+hipError_t launch_init_equilibrium(float *f, long long rows, int rf, int pitch, long long P, float c0, float c1,
+                                   float c2, hipStream_t s);
 hipError_t launch_aos_to_soa(const float *aos, float *f, long long P, int pitch, int w, int h, hipStream_t s);
 hipError_t launch_soa_to_aos(const float *f, float *aos, long long P, int pitch, int w, int h, hipStream_t s);
 hipError_t launch_halo_pack(const HaloArgs &a, hipStream_t s);
@@ -120,6 +122,7 @@ struct Sub {
     lbm_rect rect{};
     int w = 0, h = 0, pitch = 0;
     long long plane = 0;
+    long long lattice_floats = 0;
     float *f[2] = {nullptr, nullptr};
     uint8_t *obst = nullptr;
     float *halo_mem = nullptr;  // all send + recv buffers
@@ -156,6 +159,10 @@ struct lbm_handle {
     int rank = 0, world = 1;
     bool vec4 = true;
     int graph_steps = 0;
+    // tuning knobs (environment, read at create): LBM_KFLAGS (bit0 nt stores,
+    // bit1 nt loads), LBM_MIN_WAVES, LBM_MAX_BLOCKS, LBM_LAYOUT (planar|rows)
+    int kflags = 0, kwaves = 1, max_blocks_cfg = 2048;
+    bool row_interleaved = false;
     std::vector<lbm_rect> all_rects;
     std::vector<Sub> subs;  // local sub-domains
     ncclComm_t comm = nullptr;
@@ -206,10 +213,19 @@ struct lbm_handle {
         return e;
     }
 
-    int max_blocks() const {
-        const char *v = getenv("LBM_MAX_BLOCKS");
-        if (v && atoi(v) > 0) return atoi(v);
-        return 2048;
+    int max_blocks() const { return max_blocks_cfg; }
+
+    static int env_int(const char *name, int dflt) {
+        const char *v = getenv(name);
+        return (v && *v) ? atoi(v) : dflt;
+    }
+
+    void read_tuning() {
+        kflags = env_int("LBM_KFLAGS", kflags);
+        kwaves = env_int("LBM_MIN_WAVES", kwaves);
+        max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
+        const char *l = getenv("LBM_LAYOUT");
+        if (l && *l) row_interleaved = std::string(l) == "rows";
     }
 
     // rects: x0, y0 in cells; widths in cells (converted to work items here)
@@ -334,6 +350,7 @@ struct lbm_handle {
         if (!obstacles) throw lbm_failure(LBM_E_INVALID, "obstacles must not be NULL");
         parts = cfg.parts > 0 ? cfg.parts : 1;
         transport = cfg.transport;
+        read_tuning();
         graph_steps = cfg.graph_steps;
         if (partition(p.nx, p.ny, parts, cfg.grid_rows, cfg.grid_cols, R, C, all_rects) != LBM_OK)
             throw lbm_failure(LBM_E_INVALID, "cannot partition " + std::to_string(p.nx) + "x" + std::to_string(p.ny) +
@@ -426,14 +443,25 @@ struct lbm_handle {
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
         set_device(s);
-        s.pitch = (int)round_up(s.w + XOFF + 1, 64);
+        const int row_floats = (int)round_up(s.w + XOFF + 1, 64);
         const long long rows = s.h + 2;
-        // plane stride: a multiple of 64 floats plus an odd multiple of 64
-        // floats so the nine concurrent plane streams do not alias
-        s.plane = round_up(rows * s.pitch, 1024) + 320;
+        long long total_floats;
+        if (row_interleaved) {
+            // f[y][k][x]: the nine populations of a row are adjacent
+            s.plane = row_floats;
+            s.pitch = Q * row_floats;
+            total_floats = rows * s.pitch;
+        } else {
+            // f[k][y][x]: plane stride padded off a power of two so the nine
+            // concurrent plane streams do not alias
+            s.pitch = row_floats;
+            s.plane = round_up(rows * s.pitch, 1024) + 320;
+            total_floats = Q * s.plane;
+        }
+        s.lattice_floats = total_floats;
         for (int k = 0; k < 2; ++k) {
-            HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)(Q * s.plane)));
-            HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)(Q * s.plane)));
+            HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)total_floats));
+            HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)total_floats));
         }
         HIP_CHECK(hipMalloc(&s.obst, (size_t)round_up((long long)s.w * s.h + 16, 256)));
         HIP_CHECK(hipMemcpy2D(s.obst, (size_t)s.w, obstacles + (size_t)s.rect.y0 * p.nx + s.rect.x0, (size_t)p.nx,
@@ -561,7 +589,7 @@ struct lbm_handle {
     void step_once() {
         if (!multi()) {
             Sub &s = subs[0];
-            HIP_CHECK(launch_step(s.args_int[s.cur], s.n_int_blocks, vec4, true, s.s_comp));
+            HIP_CHECK(launch_step(s.args_int[s.cur], s.n_int_blocks, vec4, true, kflags, kwaves, s.s_comp));
             s.cur ^= 1;
             return;
         }
@@ -570,14 +598,14 @@ struct lbm_handle {
             Sub &s = subs[k];
             set_device(s);
             if (s.n_bnd_blocks > 0)
-                HIP_CHECK(launch_step(s.args_bnd[s.cur], s.n_bnd_blocks, vec4, false, s.s_comp));
+                HIP_CHECK(launch_step(s.args_bnd[s.cur], s.n_bnd_blocks, vec4, false, kflags, kwaves, s.s_comp));
             HIP_CHECK(hipEventRecord(s.ev_b, s.s_comp));
             unp[k] = s.unpack[s.cur];
         }
         exchange(unp.data());
         for (auto &s : subs) {
             set_device(s);
-            HIP_CHECK(launch_step(s.args_int[s.cur], s.n_int_blocks, vec4, true, s.s_comp));
+            HIP_CHECK(launch_step(s.args_int[s.cur], s.n_int_blocks, vec4, true, kflags, kwaves, s.s_comp));
         }
         wait_exchange();
         for (auto &s : subs) s.cur ^= 1;
@@ -642,7 +670,8 @@ struct lbm_handle {
         for (auto &s : subs) {
             set_device(s);
             s.cur = 0;
-            HIP_CHECK(launch_init_equilibrium(s.f[0], s.plane, c0, c1, c2, s.s_comp));
+            HIP_CHECK(launch_init_equilibrium(s.f[0], s.h + 2, (int)std::min<long long>(s.pitch, s.plane), s.pitch,
+                                              s.plane, c0, c1, c2, s.s_comp));
         }
         sync_all();
         loaded = true;

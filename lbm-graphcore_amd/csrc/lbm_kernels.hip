@@ -37,8 +37,31 @@
 
 namespace lbm {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+
+// Streaming (non-temporal) variants: the lattice is touched once per step
+// and is far larger than L2 / the Infinity Cache at the roofline sizes.
+template <bool kNT>
+__device__ __forceinline__ float4 ld4s(const float *p) {
+    if constexpr (kNT) {
+        const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return ld4(p);
+    }
+}
+template <bool kNT>
+__device__ __forceinline__ void st4s(float *p, float4 v) {
+    if constexpr (kNT) {
+        f32x4 u = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(u, reinterpret_cast<f32x4 *>(p));
+    } else {
+        st4(p, v);
+    }
+}
 
 // Bijective XCD-aware block remap (blocks b and b+8 share an XCD): blocks on
 // one XCD get consecutive logical ids, so neighbouring chunks -- which share
@@ -63,13 +86,34 @@ __device__ __forceinline__ float block_sum(float v, float *lds) {
     return r;
 }
 
+// Sum n block partials in a fixed order (depends on n only): float4 loads,
+// four independent accumulators per thread so the loads overlap, then the
+// block tree.  Result valid in thread 0.
+__device__ __forceinline__ float sum_partials(const float *p, int n, float *lds) {
+    const int n4 = n >> 2;
+    const float4 *p4 = reinterpret_cast<const float4 *>(p);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int i = threadIdx.x;
+    for (; i + 3 * BLOCK < n4; i += 4 * BLOCK) {
+        const float4 x0 = p4[i], x1 = p4[i + BLOCK], x2 = p4[i + 2 * BLOCK], x3 = p4[i + 3 * BLOCK];
+        a0 += (x0.x + x0.y) + (x0.z + x0.w);
+        a1 += (x1.x + x1.y) + (x1.z + x1.w);
+        a2 += (x2.x + x2.y) + (x2.z + x2.w);
+        a3 += (x3.x + x3.y) + (x3.z + x3.w);
+    }
+    for (; i < n4; i += BLOCK) {
+        const float4 x0 = p4[i];
+        a0 += (x0.x + x0.y) + (x0.z + x0.w);
+    }
+    for (int k = 4 * n4 + threadIdx.x; k < n; k += BLOCK) a1 += p[k];
+    return block_sum((a0 + a1) + (a2 + a3), lds);
+}
+
 // Block 0: fold the previous step's partials into av_local[ctl[1]++].
 __device__ __forceinline__ void reduce_prev(const StepArgs &a, float *lds) {
     const int pending = a.ctl[0];
     if (!pending) return;
-    float v = 0.f;
-    for (int i = threadIdx.x; i < a.n_prev; i += BLOCK) v += a.partials_prev[i];
-    const float s = block_sum(v, lds);
+    const float s = sum_partials(a.partials_prev, a.n_prev, lds);
     if (threadIdx.x == 0) {
         const int idx = a.ctl[1];
         a.av_local[idx] = s;
@@ -140,8 +184,13 @@ __device__ __forceinline__ RectPos locate(const StepArgs &a, int t, int tid) {
 // Fast path: 4 consecutive cells per lane, float4 loads/stores.
 // Requires w % 4 == 0 and every rect aligned to 4 columns.
 // --------------------------------------------------------------------------
-template <bool kReduce>
-__global__ __launch_bounds__(BLOCK) void step_vec4(StepArgs a) {
+// kFlags: bit 0 = non-temporal stores, bit 1 = non-temporal loads.
+// kMinWaves: occupancy request (waves per SIMD) passed to the register allocator.
+template <bool kReduce, int kFlags, int kMinWaves>
+__global__ __launch_bounds__(BLOCK, kMinWaves) void step_vec4(StepArgs a) {
+    constexpr bool kNTS = (kFlags & 1) != 0;
+    constexpr bool kNTL = (kFlags & 2) != 0;
+    constexpr bool kPlaneOrder = (kFlags & 4) != 0;
     __shared__ float lds[4];
     if (kReduce && blockIdx.x == 0) reduce_prev(a, lds);
 
@@ -164,15 +213,15 @@ __global__ __launch_bounds__(BLOCK) void step_vec4(StepArgs a) {
         const float *rm = r0 - pitch;                                      // row y-1
         const float *rp1 = r0 + pitch;                                     // row y+1
 
-        const float4 v0 = ld4(r0);
-        const float4 v1 = ld4(r0 + 1 * P);
-        const float4 v2 = ld4(rm + 2 * P);
-        const float4 v3 = ld4(r0 + 3 * P);
-        const float4 v4 = ld4(rp1 + 4 * P);
-        const float4 v5 = ld4(rm + 5 * P);
-        const float4 v6 = ld4(rm + 6 * P);
-        const float4 v7 = ld4(rp1 + 7 * P);
-        const float4 v8 = ld4(rp1 + 8 * P);
+        const float4 v0 = ld4s<kNTL>(r0);
+        const float4 v1 = ld4s<kNTL>(r0 + 1 * P);
+        const float4 v2 = ld4s<kNTL>(rm + 2 * P);
+        const float4 v3 = ld4s<kNTL>(r0 + 3 * P);
+        const float4 v4 = ld4s<kNTL>(rp1 + 4 * P);
+        const float4 v5 = ld4s<kNTL>(rm + 5 * P);
+        const float4 v6 = ld4s<kNTL>(rm + 6 * P);
+        const float4 v7 = ld4s<kNTL>(rp1 + 7 * P);
+        const float4 v8 = ld4s<kNTL>(rp1 + 8 * P);
         const uint32_t ob = *reinterpret_cast<const uint32_t *>(a.obst + (long long)y * a.w + x0);
 
         float e1 = 0.f, e5 = 0.f, e8 = 0.f, e3 = 0.f, e6 = 0.f, e7 = 0.f;
@@ -198,63 +247,193 @@ __global__ __launch_bounds__(BLOCK) void step_vec4(StepArgs a) {
         q7 = rdir ? e7 : q7;
 
         const float accf = (y == a.accel_row) ? 1.00f : 0.00f;
-        float o[4][Q];
-        {
-            const float s[Q] = {v0.x, l1, v2.x, v3.y, v4.x, l5, v6.y, v7.y, l8};
-            const float u = collide(s, o[0], (ob & 0xffu) != 0, accf, a.omega, a.omo, a.w1, a.w2);
-            if (active) tot += u;
-        }
-        {
-            const float s[Q] = {v0.y, v1.x, v2.y, v3.z, v4.y, v5.x, v6.z, v7.z, v8.x};
-            const float u = collide(s, o[1], (ob & 0xff00u) != 0, accf, a.omega, a.omo, a.w1, a.w2);
-            if (active) tot += u;
-        }
-        {
-            const float s[Q] = {v0.z, v1.y, v2.z, v3.w, v4.z, v5.y, v6.w, v7.w, v8.y};
-            const float u = collide(s, o[2], (ob & 0xff0000u) != 0, accf, a.omega, a.omo, a.w1, a.w2);
-            if (active) tot += u;
-        }
-        {
-            const float s[Q] = {v0.w, v1.z, v2.w, q3, v4.w, v5.z, q6, q7, v8.z};
-            const float u = collide(s, o[3], (ob & 0xff000000u) != 0, accf, a.omega, a.omo, a.w1, a.w2);
-            if (active) tot += u;
-        }
-
-        if (active) {
-            float *w0 = a.fout + (long long)(y + 1) * pitch + XOFF + x0;
+        if constexpr (kPlaneOrder) {
+            // Macroscopic values per cell first, then each plane (or rebound
+            // pair) is finished and stored, so inputs and outputs retire early.
+            const float S[Q][4] = {{v0.x, v0.y, v0.z, v0.w}, {l1, v1.x, v1.y, v1.z}, {v2.x, v2.y, v2.z, v2.w},
+                                   {v3.y, v3.z, v3.w, q3},   {v4.x, v4.y, v4.z, v4.w}, {l5, v5.x, v5.y, v5.z},
+                                   {v6.y, v6.z, v6.w, q6},   {v7.y, v7.z, v7.w, q7},   {l8, v8.x, v8.y, v8.z}};
+            float rho[4], ux[4], uy[4], csq[4], ld1[4], ld2[4];
+            bool obf[4];
 #pragma unroll
-            for (int k = 0; k < Q; ++k) st4(w0 + k * P, make_float4(o[0][k], o[1][k], o[2][k], o[3][k]));
-
-            // ---- edge populations: own ghost ring or halo send buffers ----
+            for (int j = 0; j < 4; ++j) {
+                obf[j] = ((ob >> (8 * j)) & 0xffu) != 0;
+                rho[j] = S[0][j] + S[1][j] + S[2][j] + S[3][j] + S[4][j] + S[5][j] + S[6][j] + S[7][j] + S[8][j];
+                ux[j] = (S[1][j] + S[5][j] + S[8][j] - (S[3][j] + S[6][j] + S[7][j])) / rho[j];
+                uy[j] = (S[2][j] + S[5][j] + S[6][j] - (S[4][j] + S[7][j] + S[8][j])) / rho[j];
+                const float usq = ux[j] * ux[j] + uy[j] * uy[j];
+                csq[j] = 1.00f - usq * 1.50f;
+                ld1[j] = rho[j] / 9.00f * a.omega;
+                ld2[j] = rho[j] / 36.00f * a.omega;
+                const float u = obf[j] ? 0.f : sqrtf(usq);
+                if (active) tot += u;
+            }
+            const float omo = a.omo, w1 = a.w1, w2 = a.w2;
+            float *w0 = a.fout + (long long)(y + 1) * pitch + XOFF + x0;
             const bool east = (x0 + 3 == a.w - 1), west = (x0 == 0);
             const bool north = (y == a.h - 1), south = (y == 0);
-            if (east) {
-                const EdgeDst &d = a.dst[DE];
-                d.p[0][y * d.ps] = o[3][1];
-                d.p[1][y * d.ps] = o[3][5];
-                d.p[2][y * d.ps] = o[3][8];
+            float4 ok;
+            // plane 0
+            {
+                float o[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    o[j] = obf[j] ? S[0][j] : S[0][j] * omo + 4.00f / 9.00f * rho[j] * a.omega * csq[j];
+                ok = make_float4(o[0], o[1], o[2], o[3]);
+                if (active) st4s<kNTS>(w0, ok);
             }
-            if (west) {
-                const EdgeDst &d = a.dst[DW];
-                d.p[0][y * d.ps] = o[0][3];
-                d.p[1][y * d.ps] = o[0][6];
-                d.p[2][y * d.ps] = o[0][7];
+            // E / W pair
+            {
+                float o1[4], o3[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float c1 = S[1][j] * omo + ld1[j] * ((4.50f * ux[j]) * (2.00f / 3.00f + ux[j]) + csq[j]);
+                    const float c3 = S[3][j] * omo + ld1[j] * ((-4.50f * ux[j]) * (2.00f / 3.00f - ux[j]) + csq[j]);
+                    o1[j] = obf[j] ? S[3][j] : c1 + accf * w1;
+                    o3[j] = obf[j] ? S[1][j] : c3 - accf * w1;
+                }
+                if (active) {
+                    st4s<kNTS>(w0 + 1 * P, make_float4(o1[0], o1[1], o1[2], o1[3]));
+                    st4s<kNTS>(w0 + 3 * P, make_float4(o3[0], o3[1], o3[2], o3[3]));
+                    if (east) a.dst[DE].p[0][y * a.dst[DE].ps] = o1[3];
+                    if (west) a.dst[DW].p[0][y * a.dst[DW].ps] = o3[0];
+                }
             }
-            if (north) {
-                const EdgeDst &d = a.dst[DN];
-                st4(d.p[0] + x0, make_float4(o[0][2], o[1][2], o[2][2], o[3][2]));
-                st4(d.p[1] + x0, make_float4(o[0][5], o[1][5], o[2][5], o[3][5]));
-                st4(d.p[2] + x0, make_float4(o[0][6], o[1][6], o[2][6], o[3][6]));
-                if (east) a.dst[DNE].p[0][0] = o[3][5];
-                if (west) a.dst[DNW].p[0][0] = o[0][6];
+            // N / S pair
+            {
+                float o2[4], o4[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float c2 = S[2][j] * omo + ld1[j] * ((4.50f * uy[j]) * (2.00f / 3.00f + uy[j]) + csq[j]);
+                    const float c4 = S[4][j] * omo + ld1[j] * ((-4.50f * uy[j]) * (2.00f / 3.00f - uy[j]) + csq[j]);
+                    o2[j] = obf[j] ? S[4][j] : c2;
+                    o4[j] = obf[j] ? S[2][j] : c4;
+                }
+                const float4 k2 = make_float4(o2[0], o2[1], o2[2], o2[3]);
+                const float4 k4 = make_float4(o4[0], o4[1], o4[2], o4[3]);
+                if (active) {
+                    st4s<kNTS>(w0 + 2 * P, k2);
+                    st4s<kNTS>(w0 + 4 * P, k4);
+                    if (north) st4(a.dst[DN].p[0] + x0, k2);
+                    if (south) st4(a.dst[DS].p[0] + x0, k4);
+                }
             }
-            if (south) {
-                const EdgeDst &d = a.dst[DS];
-                st4(d.p[0] + x0, make_float4(o[0][4], o[1][4], o[2][4], o[3][4]));
-                st4(d.p[1] + x0, make_float4(o[0][7], o[1][7], o[2][7], o[3][7]));
-                st4(d.p[2] + x0, make_float4(o[0][8], o[1][8], o[2][8], o[3][8]));
-                if (west) a.dst[DSW].p[0][0] = o[0][7];
-                if (east) a.dst[DSE].p[0][0] = o[3][8];
+            // NE / SW pair
+            {
+                float o5[4], o7[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float us = ux[j] + uy[j];
+                    const float c5 = S[5][j] * omo + ld2[j] * ((4.50f * us) * (2.00f / 3.00f + us) + csq[j]);
+                    const float c7 = S[7][j] * omo + ld2[j] * ((-4.50f * us) * (2.00f / 3.00f - us) + csq[j]);
+                    o5[j] = obf[j] ? S[7][j] : c5 + accf * w2;
+                    o7[j] = obf[j] ? S[5][j] : c7 - accf * w2;
+                }
+                const float4 k5 = make_float4(o5[0], o5[1], o5[2], o5[3]);
+                const float4 k7 = make_float4(o7[0], o7[1], o7[2], o7[3]);
+                if (active) {
+                    st4s<kNTS>(w0 + 5 * P, k5);
+                    st4s<kNTS>(w0 + 7 * P, k7);
+                    if (east) a.dst[DE].p[1][y * a.dst[DE].ps] = o5[3];
+                    if (west) a.dst[DW].p[2][y * a.dst[DW].ps] = o7[0];
+                    if (north) {
+                        st4(a.dst[DN].p[1] + x0, k5);
+                        if (east) a.dst[DNE].p[0][0] = o5[3];
+                    }
+                    if (south) {
+                        st4(a.dst[DS].p[1] + x0, k7);
+                        if (west) a.dst[DSW].p[0][0] = o7[0];
+                    }
+                }
+            }
+            // NW / SE pair
+            {
+                float o6[4], o8[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float ud = -ux[j] + uy[j];
+                    const float c6 = S[6][j] * omo + ld2[j] * ((4.50f * ud) * (2.00f / 3.00f + ud) + csq[j]);
+                    const float c8 = S[8][j] * omo + ld2[j] * ((-4.50f * ud) * (2.00f / 3.00f - ud) + csq[j]);
+                    o6[j] = obf[j] ? S[8][j] : c6 - accf * w2;
+                    o8[j] = obf[j] ? S[6][j] : c8 + accf * w2;
+                }
+                const float4 k6 = make_float4(o6[0], o6[1], o6[2], o6[3]);
+                const float4 k8 = make_float4(o8[0], o8[1], o8[2], o8[3]);
+                if (active) {
+                    st4s<kNTS>(w0 + 6 * P, k6);
+                    st4s<kNTS>(w0 + 8 * P, k8);
+                    if (east) a.dst[DE].p[2][y * a.dst[DE].ps] = o8[3];
+                    if (west) a.dst[DW].p[1][y * a.dst[DW].ps] = o6[0];
+                    if (north) {
+                        st4(a.dst[DN].p[2] + x0, k6);
+                        if (west) a.dst[DNW].p[0][0] = o6[0];
+                    }
+                    if (south) {
+                        st4(a.dst[DS].p[2] + x0, k8);
+                        if (east) a.dst[DSE].p[0][0] = o8[3];
+                    }
+                }
+            }
+            (void)ok;
+        } else {
+            float o[4][Q];
+            {
+                const float s[Q] = {v0.x, l1, v2.x, v3.y, v4.x, l5, v6.y, v7.y, l8};
+                const float u = collide(s, o[0], (ob & 0xffu) != 0, accf, a.omega, a.omo, a.w1, a.w2);
+                if (active) tot += u;
+            }
+            {
+                const float s[Q] = {v0.y, v1.x, v2.y, v3.z, v4.y, v5.x, v6.z, v7.z, v8.x};
+                const float u = collide(s, o[1], (ob & 0xff00u) != 0, accf, a.omega, a.omo, a.w1, a.w2);
+                if (active) tot += u;
+            }
+            {
+                const float s[Q] = {v0.z, v1.y, v2.z, v3.w, v4.z, v5.y, v6.w, v7.w, v8.y};
+                const float u = collide(s, o[2], (ob & 0xff0000u) != 0, accf, a.omega, a.omo, a.w1, a.w2);
+                if (active) tot += u;
+            }
+            {
+                const float s[Q] = {v0.w, v1.z, v2.w, q3, v4.w, v5.z, q6, q7, v8.z};
+                const float u = collide(s, o[3], (ob & 0xff000000u) != 0, accf, a.omega, a.omo, a.w1, a.w2);
+                if (active) tot += u;
+            }
+
+            if (active) {
+                float *w0 = a.fout + (long long)(y + 1) * pitch + XOFF + x0;
+#pragma unroll
+                for (int k = 0; k < Q; ++k) st4s<kNTS>(w0 + k * P, make_float4(o[0][k], o[1][k], o[2][k], o[3][k]));
+
+                // ---- edge populations: own ghost ring or halo send buffers ----
+                const bool east = (x0 + 3 == a.w - 1), west = (x0 == 0);
+                const bool north = (y == a.h - 1), south = (y == 0);
+                if (east) {
+                    const EdgeDst &d = a.dst[DE];
+                    d.p[0][y * d.ps] = o[3][1];
+                    d.p[1][y * d.ps] = o[3][5];
+                    d.p[2][y * d.ps] = o[3][8];
+                }
+                if (west) {
+                    const EdgeDst &d = a.dst[DW];
+                    d.p[0][y * d.ps] = o[0][3];
+                    d.p[1][y * d.ps] = o[0][6];
+                    d.p[2][y * d.ps] = o[0][7];
+                }
+                if (north) {
+                    const EdgeDst &d = a.dst[DN];
+                    st4(d.p[0] + x0, make_float4(o[0][2], o[1][2], o[2][2], o[3][2]));
+                    st4(d.p[1] + x0, make_float4(o[0][5], o[1][5], o[2][5], o[3][5]));
+                    st4(d.p[2] + x0, make_float4(o[0][6], o[1][6], o[2][6], o[3][6]));
+                    if (east) a.dst[DNE].p[0][0] = o[3][5];
+                    if (west) a.dst[DNW].p[0][0] = o[0][6];
+                }
+                if (south) {
+                    const EdgeDst &d = a.dst[DS];
+                    st4(d.p[0] + x0, make_float4(o[0][4], o[1][4], o[2][4], o[3][4]));
+                    st4(d.p[1] + x0, make_float4(o[0][7], o[1][7], o[2][7], o[3][7]));
+                    st4(d.p[2] + x0, make_float4(o[0][8], o[1][8], o[2][8], o[3][8]));
+                    if (west) a.dst[DSW].p[0][0] = o[0][7];
+                    if (east) a.dst[DSE].p[0][0] = o[3][8];
+                }
             }
         }
     }
@@ -343,9 +522,7 @@ __global__ __launch_bounds__(BLOCK) void step_scalar(StepArgs a) {
 __global__ __launch_bounds__(BLOCK) void finalize_av(const float *partials, int n, float *av_local, int *ctl) {
     __shared__ float lds[4];
     if (ctl[0] == 0) return;
-    float v = 0.f;
-    for (int i = threadIdx.x; i < n; i += BLOCK) v += partials[i];
-    const float s = block_sum(v, lds);
+    const float s = sum_partials(partials, n, lds);
     if (threadIdx.x == 0) {
         const int idx = ctl[1];
         av_local[idx] = s;
@@ -372,20 +549,23 @@ __global__ __launch_bounds__(BLOCK) void accelerate_row(float *f, const uint8_t 
     }
 }
 
-// Equilibrium at rest over the whole allocation, ghosts included
-// (LatticeBoltzmannUtils.hpp:137-157).
-__global__ __launch_bounds__(BLOCK) void init_equilibrium(float *f, long long P, float c0, float c1, float c2) {
+// Equilibrium at rest over every row of the allocation, ghosts included
+// (LatticeBoltzmannUtils.hpp:137-157).  rf = floats per plane row.
+__global__ __launch_bounds__(BLOCK) void init_equilibrium(float *f, long long rows, int rf, int pitch, long long P,
+                                                         float c0, float c1, float c2) {
     const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= P) return;
-    f[i] = c0;
-    f[1 * P + i] = c1;
-    f[2 * P + i] = c1;
-    f[3 * P + i] = c1;
-    f[4 * P + i] = c1;
-    f[5 * P + i] = c2;
-    f[6 * P + i] = c2;
-    f[7 * P + i] = c2;
-    f[8 * P + i] = c2;
+    if (i >= rows * rf) return;
+    const long long r = i / rf, x = i - r * rf;
+    float *d = f + r * pitch + x;
+    d[0] = c0;
+    d[1 * P] = c1;
+    d[2 * P] = c1;
+    d[3 * P] = c1;
+    d[4 * P] = c1;
+    d[5 * P] = c2;
+    d[6 * P] = c2;
+    d[7 * P] = c2;
+    d[8 * P] = c2;
 }
 
 // AoS [h][w][9] staging <-> SoA ghosted lattice.
@@ -478,12 +658,36 @@ __global__ __launch_bounds__(BLOCK) void halo_unpack(HaloArgs a) {
 
 // ---- host-side launch wrappers (called from lbm_engine.hip) ---------------
 
-hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hipStream_t s) {
+template <bool R, int F>
+static void launch_vec4_w(const StepArgs &a, int blocks, int min_waves, hipStream_t s) {
+    switch (min_waves) {
+        case 5: hipLaunchKernelGGL((step_vec4<R, F, 5>), dim3(blocks), dim3(BLOCK), 0, s, a); break;
+        case 6: hipLaunchKernelGGL((step_vec4<R, F, 6>), dim3(blocks), dim3(BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((step_vec4<R, F, 1>), dim3(blocks), dim3(BLOCK), 0, s, a); break;
+    }
+}
+
+template <bool R>
+static void launch_vec4_f(const StepArgs &a, int blocks, int flags, int min_waves, hipStream_t s) {
+    switch (flags & 7) {
+        case 1: launch_vec4_w<R, 1>(a, blocks, min_waves, s); break;
+        case 2: launch_vec4_w<R, 2>(a, blocks, min_waves, s); break;
+        case 3: launch_vec4_w<R, 3>(a, blocks, min_waves, s); break;
+        case 4: launch_vec4_w<R, 4>(a, blocks, min_waves, s); break;
+        case 5: launch_vec4_w<R, 5>(a, blocks, min_waves, s); break;
+        case 6: launch_vec4_w<R, 6>(a, blocks, min_waves, s); break;
+        case 7: launch_vec4_w<R, 7>(a, blocks, min_waves, s); break;
+        default: launch_vec4_w<R, 0>(a, blocks, min_waves, s); break;
+    }
+}
+
+hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, int flags, int min_waves,
+                       hipStream_t s) {
     if (vec4) {
         if (reduce)
-            hipLaunchKernelGGL(step_vec4<true>, dim3(blocks), dim3(BLOCK), 0, s, a);
+            launch_vec4_f<true>(a, blocks, flags, min_waves, s);
         else
-            hipLaunchKernelGGL(step_vec4<false>, dim3(blocks), dim3(BLOCK), 0, s, a);
+            launch_vec4_f<false>(a, blocks, flags, min_waves, s);
     } else {
         if (reduce)
             hipLaunchKernelGGL(step_scalar<true>, dim3(blocks), dim3(BLOCK), 0, s, a);
@@ -505,9 +709,11 @@ hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pit
     return hipGetLastError();
 }
 
-hipError_t launch_init_equilibrium(float *f, long long P, float c0, float c1, float c2, hipStream_t s) {
-    hipLaunchKernelGGL(init_equilibrium, dim3((unsigned)((P + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, f, P, c0, c1,
-                       c2);
+hipError_t launch_init_equilibrium(float *f, long long rows, int rf, int pitch, long long P, float c0, float c1,
+                                   float c2, hipStream_t s) {
+    const long long n = rows * rf;
+    hipLaunchKernelGGL(init_equilibrium, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, f, rows, rf,
+                       pitch, P, c0, c1, c2);
     return hipGetLastError();
 }
 

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""A/B the step kernel's tuning knobs in ONE process (interleaved rounds).
+
+Each variant is a set of LBM_* environment knobs read by lbm_create_ex
+(LBM_LAYOUT, LBM_KFLAGS, LBM_MIN_WAVES, LBM_MAX_BLOCKS).  For every round,
+every variant creates an engine on the same synthetic problem, warms up and
+times `steps` steps with the library's device events.  Prints one JSON line
+per variant with the median / min ms per step and GB/s (72 B per update).
+
+  python tools/ab_bench.py --n 8192 --steps 100 --rounds 3 \
+      --variant base: --variant rows:LBM_LAYOUT=rows --variant nt:LBM_KFLAGS=1
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "lbm-graphcore_amd")]
+
+from lbm_amd import io as lio  # noqa: E402
+from lbm_amd import native  # noqa: E402
+from bench import synthetic_obstacles  # noqa: E402
+
+KNOBS = ["LBM_LAYOUT", "LBM_KFLAGS", "LBM_MIN_WAVES", "LBM_MAX_BLOCKS"]
+
+
+def parse_variant(s: str):
+    name, _, rest = s.partition(":")
+    env = {}
+    for kv in filter(None, rest.split(",")):
+        k, _, v = kv.partition("=")
+        env[k] = v
+    return name, env
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--ny", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variant", action="append", default=[])
+    ap.add_argument("--check", action="store_true", help="also compare each variant's lattice to the first")
+    a = ap.parse_args()
+    nx, ny = a.n, a.ny or a.n
+    p = lio.Params(nx, ny, a.steps, 10, 0.1, 0.005, 1.85)
+    obst = synthetic_obstacles(nx, ny)
+    variants = [parse_variant(v) for v in (a.variant or ["base:"])]
+    times = {name: [] for name, _ in variants}
+    ref = None
+    for rnd in range(a.rounds):
+        for name, env in variants:
+            for k in KNOBS:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            with native.Engine(p, obst, devices=[0]) as e:
+                e.init_equilibrium()
+                e.run_steps(a.warmup, accelerate_first=True)
+                e.run_steps(a.steps)
+                times[name].append(e.last_run_seconds() / a.steps)
+                if a.check and rnd == 0:
+                    cells, _ = e.store(n_av=1)
+                    if ref is None:
+                        ref = cells
+                    elif not (cells == ref).all():
+                        print(json.dumps({"variant": name, "error": "lattice differs from first variant"}))
+    for name, env in variants:
+        ts = times[name]
+        med = statistics.median(ts)
+        print(json.dumps({"variant": name, "env": env, "grid": f"{nx}x{ny}", "ms_median": round(med * 1e3, 4),
+                          "ms_min": round(min(ts) * 1e3, 4),
+                          "gbs_median": round(72 * nx * ny / med / 1e9, 1),
+                          "mlups_median": round(nx * ny / med / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
