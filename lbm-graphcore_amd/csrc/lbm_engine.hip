@@ -161,8 +161,10 @@ struct lbm_handle {
     int graph_steps = 0;
     // tuning knobs (environment, read at create): LBM_KFLAGS (bit0 nt stores,
     // bit1 nt loads), LBM_MIN_WAVES, LBM_MAX_BLOCKS, LBM_LAYOUT (planar|rows)
-    int kflags = 0, kwaves = 1, max_blocks_cfg = 2048;
-    bool row_interleaved = false;
+    // defaults chosen by tools/ab_bench.py on MI355X (profiles/r01/ab_*.log):
+    // plane-ordered kernel, row-interleaved f[y][k][x], one tile per block
+    int kflags = 4, kwaves = 1, max_blocks_cfg = 1 << 30;
+    bool row_interleaved = true;
     std::vector<lbm_rect> all_rects;
     std::vector<Sub> subs;  // local sub-domains
     ncclComm_t comm = nullptr;
@@ -225,7 +227,7 @@ struct lbm_handle {
         kwaves = env_int("LBM_MIN_WAVES", kwaves);
         max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
         const char *l = getenv("LBM_LAYOUT");
-        if (l && *l) row_interleaved = std::string(l) == "rows";
+        if (l && *l) row_interleaved = std::string(l) != "planar";
     }
 
     // rects: x0, y0 in cells; widths in cells (converted to work items here)
