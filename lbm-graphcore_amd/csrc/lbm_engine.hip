@@ -159,6 +159,8 @@ struct lbm_handle {
     int rank = 0, world = 1;
     bool vec4 = true;
     int graph_steps = 0;
+    // hipGraph of 2*graph_steps single-sub-domain steps, one per starting parity
+    hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
     // tuning knobs (environment, read at create): LBM_KFLAGS (bit0 nt stores,
     // bit1 nt loads), LBM_MIN_WAVES, LBM_MAX_BLOCKS, LBM_LAYOUT (planar|rows)
     // defaults chosen by tools/ab_bench.py on MI355X (profiles/r01/ab_*.log):
@@ -226,6 +228,7 @@ struct lbm_handle {
         kflags = env_int("LBM_KFLAGS", kflags);
         kwaves = env_int("LBM_MIN_WAVES", kwaves);
         max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
+        graph_steps = std::max(0, env_int("LBM_GRAPH_STEPS", graph_steps));
         const char *l = getenv("LBM_LAYOUT");
         if (l && *l) row_interleaved = std::string(l) != "planar";
     }
@@ -333,6 +336,7 @@ struct lbm_handle {
     void ensure_av(int n) {
         for (auto &s : subs) {
             if (s.av_cap >= n) continue;
+            drop_graphs();
             set_device(s);
             if (s.av_local) HIP_CHECK(hipFree(s.av_local));
             s.av_cap = std::max(n, 1);
@@ -613,6 +617,44 @@ struct lbm_handle {
         for (auto &s : subs) s.cur ^= 1;
     }
 
+    void drop_graphs() {
+        for (auto &g : graph_exec)
+            if (g) {
+                (void)hipGraphExecDestroy(g);
+                g = nullptr;
+            }
+    }
+
+    // Capture 2*graph_steps steps starting at parity `par` (single sub-domain):
+    // the launch-bound small grids replay them instead of paying a host
+    // launch per step.  Kernel arguments are per parity and the av index is
+    // device-side, so one graph serves every replay.
+    hipGraphExec_t graph_for(int par) {
+        if (graph_exec[par]) return graph_exec[par];
+        Sub &s = subs[0];
+        set_device(s);
+        hipGraph_t g = nullptr;
+        HIP_CHECK(hipStreamBeginCapture(s.s_comp, hipStreamCaptureModeThreadLocal));
+        int cur = par;
+        for (int i = 0; i < 2 * graph_steps; ++i) {
+            const hipError_t e = launch_step(s.args_int[cur], s.n_int_blocks, vec4, true, kflags, kwaves, s.s_comp);
+            if (e != hipSuccess) {
+                hipGraph_t junk = nullptr;
+                (void)hipStreamEndCapture(s.s_comp, &junk);
+                if (junk) (void)hipGraphDestroy(junk);
+                HIP_CHECK(e);
+            }
+            cur ^= 1;
+        }
+        HIP_CHECK(hipStreamEndCapture(s.s_comp, &g));
+        hipGraphExec_t ge = nullptr;
+        const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIP_CHECK(e);
+        graph_exec[par] = ge;
+        return ge;
+    }
+
     void run_steps(int steps, bool accelerate_first) {
         if (!loaded) throw lbm_failure(LBM_E_STATE, "lattice not initialised (call lbm_load_cells or lbm_init_equilibrium)");
         if (steps < 0) throw lbm_failure(LBM_E_INVALID, "steps must be >= 0");
@@ -623,6 +665,9 @@ struct lbm_handle {
             HIP_CHECK(hipStreamSynchronize(s.s_comp));
         }
         if (multi()) sync_all();
+        const int chunk = 2 * graph_steps;
+        const bool use_graph = !multi() && graph_steps > 0 && steps >= chunk;
+        if (use_graph) (void)graph_for(subs[0].cur);  // capture + instantiate outside the timed region
         Sub &s0 = subs[0];
         set_device(s0);
         HIP_CHECK(hipEventRecord(t0, s0.s_comp));
@@ -641,7 +686,12 @@ struct lbm_handle {
             }
             refresh_halos();
         }
-        for (int t = 0; t < steps; ++t) step_once();
+        int t = 0;
+        if (use_graph) {
+            hipGraphExec_t ge = graph_for(s0.cur);  // even chunk: parity unchanged per replay
+            for (; t + chunk <= steps; t += chunk) HIP_CHECK(hipGraphLaunch(ge, s0.s_comp));
+        }
+        for (; t < steps; ++t) step_once();
         for (auto &s : subs) {
             set_device(s);
             const int np = s.n_int_blocks + s.n_bnd_blocks;
@@ -749,6 +799,7 @@ struct lbm_handle {
     }
 
     void destroy() {
+        drop_graphs();
         for (auto &s : subs) {
             if (hipSetDevice(s.dev) != hipSuccess) continue;
             (void)hipDeviceSynchronize();

@@ -14,6 +14,7 @@
 // of --device ipumodel: exercises the multi-GPU halo path on one device).
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <iomanip>
 #include <iostream>
 #include <string>
@@ -34,14 +35,16 @@ void usage(const char *exe) {
               << "      --obstacles arg  filename of obstacles file\n"
               << "      --runs arg       timed re-runs after the first (default: 5)\n"
               << "      --kernel arg     auto, scalar or vec4 (default: auto)\n"
-              << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n";
+              << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n"
+              << "      --graph-steps arg  replay the step loop as hipGraphs of 2*arg steps (default: 0 = off)\n"
+              << "      --dump-partitioning arg  write the sub-domain decomposition as JSON\n";
 }
 
 }  // namespace
 
 int main(int argc, char *argv[]) {
-    std::string paramsFile, obstaclesFile, device = "gpu", exeFile, kernel = "auto", outDir = ".";
-    int numGpus = 1, runs = 5;
+    std::string paramsFile, obstaclesFile, device = "gpu", exeFile, kernel = "auto", outDir = ".", dumpFile;
+    int numGpus = 1, runs = 5, graphSteps = 0;
     bool debug = false;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -78,6 +81,11 @@ int main(int argc, char *argv[]) {
             if (!next(kernel)) { usage(argv[0]); return EXIT_FAILURE; }
         } else if (a == "--out-dir") {
             if (!next(outDir)) { usage(argv[0]); return EXIT_FAILURE; }
+        } else if (a == "--graph-steps") {
+            if (!next(v)) { usage(argv[0]); return EXIT_FAILURE; }
+            graphSteps = std::atoi(v.c_str());
+        } else if (a == "--dump-partitioning") {
+            if (!next(dumpFile)) { usage(argv[0]); return EXIT_FAILURE; }
         } else if (a == "-h" || a == "--help") {
             usage(argv[0]);
             return EXIT_SUCCESS;
@@ -101,6 +109,33 @@ int main(int argc, char *argv[]) {
     if (!obstacles.has_value()) {
         std::cerr << "Could not parse obstacles file" << std::endl;
         return EXIT_FAILURE;
+    }
+    if (!dumpFile.empty()) {
+        // partitioning.json in the layout of grids::serializeToJson
+        // (StructuredGridUtils.hpp:135-158), one entry per GPU sub-domain;
+        // tile/worker are always 0 here.  Unlike the reference writer the
+        // "slice" object is closed, so the file is valid JSON.
+        std::vector<lbm_rect> rects(numGpus);
+        int32_t R = 0, C = 0;
+        if (lbm_partition((int32_t)params->nx, (int32_t)params->ny, numGpus, 0, 0, &R, &C, rects.data()) != LBM_OK) {
+            std::cerr << "Cannot partition the grid into " << numGpus << " parts" << std::endl;
+            return EXIT_FAILURE;
+        }
+        std::ofstream f(dumpFile);
+        f << R"({"GridPartitioning" : [)" << "\n";
+        for (int i = 0; i < numGpus; ++i) {
+            if (i) f << ",\n";
+            f << "  {\n";
+            f << "    \"ipu\":" << i << ",\n";
+            f << "    \"tile\":" << 0 << ",\n";
+            f << "    \"worker\":" << 0 << ",\n";
+            f << "    \"slice\": {\n";
+            f << "       \"rows\" : { \"from\" : " << rects[i].y0 << ",\"to\" : " << rects[i].y0 + rects[i].h << "},\n";
+            f << "       \"cols\" : { \"from\" : " << rects[i].x0 << ",\"to\" : " << rects[i].x0 + rects[i].w << "}\n";
+            f << "    }\n  }";
+        }
+        f << "\n]}\n";
+        std::cout << "Wrote " << R << "x" << C << " decomposition to " << dumpFile << std::endl;
     }
     const int ndev = lbm_device_count();
     if (ndev <= 0) {
@@ -127,6 +162,7 @@ int main(int argc, char *argv[]) {
         cfg.devices = devs.empty() ? nullptr : devs.data();
         cfg.num_devices = (int32_t)devs.size();
         cfg.kernel = kernel == "scalar" ? LBM_KERNEL_SCALAR : (kernel == "vec4" ? LBM_KERNEL_VEC4 : LBM_KERNEL_AUTO);
+        cfg.graph_steps = graphSteps;
         lbmhost::check(lbm_create_ex(&abi, obstacles->data.data(), &cfg, &h), nullptr, "lbm_create_ex");
     });
     if (debug) {

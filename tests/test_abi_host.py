@@ -200,3 +200,19 @@ def test_check_restatement(tmp_path):
     args = ["--ref-av-vels-file", str(tmp_path / "a.dat"), "--ref-final-state-file", str(tmp_path / "f.dat"),
             "--av-vels-file", str(tmp_path / "a.dat"), "--final-state-file", str(tmp_path / "f.dat")]
     assert lcheck.main(args) == 0
+
+
+def test_runner_partition_dump(tmp_path):
+    import json
+    exe = PKG / "build" / "lbm_runner"
+    out = tmp_path / "partitioning.json"
+    subprocess.run([str(exe), "--params", str(GOLD / "params" / "input_128x256.params"), "--obstacles",
+                    str(GOLD / "params" / "obstacles_128x256.dat"), "-n", "8", "--dump-partitioning", str(out)],
+                   capture_output=True, text=True)
+    d = json.loads(out.read_text())["GridPartitioning"]
+    assert len(d) == 8
+    _, _, rects = native.partition(128, 256, 8)
+    for i, e in enumerate(d):
+        x0, y0, w, h = rects[i]
+        assert e["ipu"] == i and e["slice"]["rows"] == {"from": y0, "to": y0 + h}
+        assert e["slice"]["cols"] == {"from": x0, "to": x0 + w}

@@ -1,0 +1,78 @@
+"""GPU end-to-end through the host CLIs (the reference's own entry points):
+lbm_runner (LbmRunner.cpp flags) and compare_lbm (LastChance.cpp positional
+CLI), gated with the check.py restatement against the reference's
+check/*.dat fixtures; plus hipGraph replay parity."""
+from __future__ import annotations
+
+import gzip
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, PKG, load_problem, oracle_manifest
+from lbm_amd import check as lcheck
+from lbm_amd import io as lio
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _gate(tmp_path, grid):
+    return lcheck.compare(GOLD / "check" / f"{grid}.av_vels.dat.gz", GOLD / "check" / f"{grid}.final_state.dat.gz",
+                          tmp_path / "av_vels.dat", tmp_path / "final_state.dat", 1.0)
+
+
+@pytest.mark.parametrize("args", [["-n", "1"], ["-n", "4", "--device", "loopback"],
+                                  ["-n", "1", "--graph-steps", "50"], ["-n", "2", "--device", "loopback",
+                                                                      "--kernel", "scalar"]])
+def test_lbm_runner_128(gpu_lib, tmp_path, args):
+    exe = PKG / "build" / "lbm_runner"
+    r = subprocess.run([str(exe), "--params", str(GOLD / "params" / "input_128x128.params"),
+                        "--obstacles", str(GOLD / "params" / "obstacles_128x128.dat"), "--runs", "1",
+                        "--out-dir", str(tmp_path), "--exe", "ignored.poplar", "-d"] + args,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert "==done==" in r.stdout and "Reynolds number:" in r.stdout and "MLUPS:" in r.stdout
+    re_out = float(re.search(r"Reynolds number:\s+(\S+)", r.stdout).group(1))
+    assert re_out == pytest.approx(oracle_manifest("128x128")["reynolds_last_av"], rel=2e-4)
+    res = _gate(tmp_path, "128x128")
+    assert res["passed"], res
+
+
+def test_compare_lbm_128x256(gpu_lib, tmp_path):
+    exe = PKG / "build" / "compare_lbm"
+    r = subprocess.run([str(exe), str(GOLD / "params" / "input_128x256.params"),
+                        str(GOLD / "params" / "obstacles_128x256.dat")], capture_output=True, text=True,
+                       cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr
+    m = re.search(r"Reynolds number:\s+(\S+)", r.stdout)
+    assert float(m.group(1)) == pytest.approx(oracle_manifest("128x256")["reynolds_final_state"], rel=1e-6)
+    res = _gate(tmp_path, "128x256")
+    assert res["passed"], res
+    # LastChance prints %.12E: same format as the reference's fixtures
+    first = (tmp_path / "av_vels.dat").read_text().splitlines()[0]
+    ref_first = gzip.decompress((GOLD / "check" / "128x256.av_vels.dat.gz").read_bytes()).decode().splitlines()[0]
+    assert re.fullmatch(r"0:\t\d\.\d{12}E[-+]\d\d", first) and first.split("\t")[1][:6] == ref_first.split("\t")[1][:6]
+
+
+@pytest.mark.parametrize("graph_steps", [1, 8, 64])
+def test_graph_replay_bitwise(gpu_lib, graph_steps):
+    p, obst = load_problem("128x128", iters=301)
+    cells0 = lio.init_cells(p)
+    with gpu_lib.Engine(p, obst, graph_steps=graph_steps) as e:
+        e.load_cells(cells0)
+        e.run()
+        e.run_steps(17)
+        cells, av = e.store(n_av=17)
+    c1, _ = oracle.run(p, obst, 301, cells0)  # lbm_run: accelerate + 301 steps
+    p2 = p.with_iters(17)                       # then 17 plain steps (no accelerate)
+    cur = c1.copy()
+    avs = []
+    free = oracle.free_cells(p, obst)
+    for _ in range(17):
+        cur, tot = oracle.step(p2, cur, obst)
+        avs.append(tot / free)
+    assert np.array_equal(cells, cur)
+    np.testing.assert_allclose(av, np.array(avs, np.float32), rtol=1e-5)
