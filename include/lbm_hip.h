@@ -81,8 +81,15 @@ typedef struct lbm_config {
     int32_t num_devices;
     const uint8_t *rccl_unique_id; /* 128 bytes, RCCL only */
     int32_t kernel;         /* LBM_KERNEL_* */
-    int32_t graph_steps;    /* >0: replay the step loop as hipGraphs of this many steps (single sub-domain) */
+    int32_t graph_steps;    /* >0: replay the step loop as hipGraphs of 2*graph_steps steps
+                               (single sub-domain without exchange); <0: off; 0: library default */
+    int32_t flags;          /* LBM_FLAG_* */
 } lbm_config;
+
+/* Route the periodic wrap of undecomposed dimensions through the transport
+ * too (send to / receive from itself) instead of writing the ghost ring
+ * in-kernel.  Lets one GPU exercise the full exchange path, RCCL included. */
+#define LBM_FLAG_FORCE_EXCHANGE 1
 
 typedef struct lbm_handle lbm_handle;
 

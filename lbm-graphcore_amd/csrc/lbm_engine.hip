@@ -158,7 +158,7 @@ struct lbm_handle {
     int transport = LBM_TRANSPORT_LOCAL;
     int rank = 0, world = 1;
     bool vec4 = true;
-    int graph_steps = 0;
+    int graph_steps = 8;  // default: replay 16-step graphs on the single-domain path
     // hipGraph of 2*graph_steps single-sub-domain steps, one per starting parity
     hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
     // tuning knobs (environment, read at create): LBM_KFLAGS (bit0 nt stores,
@@ -176,7 +176,9 @@ struct lbm_handle {
     double last_seconds = 0.0;
     hipEvent_t t0 = nullptr, t1 = nullptr;
     std::string err;
-    bool multi() const { return parts > 1; }
+    bool force_exchange = false;
+    // any direction goes through the transport (several sub-domains, or forced)
+    bool multi() const { return parts > 1 || force_exchange; }
 
     // ------------------------------------------------------------------
     void set_device(const Sub &s) const { HIP_CHECK(hipSetDevice(s.dev)); }
@@ -356,8 +358,10 @@ struct lbm_handle {
         if (!obstacles) throw lbm_failure(LBM_E_INVALID, "obstacles must not be NULL");
         parts = cfg.parts > 0 ? cfg.parts : 1;
         transport = cfg.transport;
-        read_tuning();
-        graph_steps = cfg.graph_steps;
+        read_tuning();  // environment knobs first; explicit config wins
+        if (cfg.graph_steps > 0) graph_steps = cfg.graph_steps;
+        if (cfg.graph_steps < 0) graph_steps = 0;
+        force_exchange = (cfg.flags & LBM_FLAG_FORCE_EXCHANGE) != 0 || env_int("LBM_FORCE_EXCHANGE", 0) != 0;
         if (partition(p.nx, p.ny, parts, cfg.grid_rows, cfg.grid_cols, R, C, all_rects) != LBM_OK)
             throw lbm_failure(LBM_E_INVALID, "cannot partition " + std::to_string(p.nx) + "x" + std::to_string(p.ny) +
                                                  " into " + std::to_string(parts) + " parts");
@@ -410,7 +414,7 @@ struct lbm_handle {
                 const int r = ((s.row + DIR_Y[d]) % R + R) % R;
                 const int c = ((s.col + DIR_X[d]) % C + C) % C;
                 s.nb[d] = r * C + c;
-                s.remote[d] = s.nb[d] != s.id;
+                s.remote[d] = force_exchange || s.nb[d] != s.id;
             }
             const int gy = p.ny - 2;
             s.accel_row = (p.ny >= 2 && gy >= s.rect.y0 && gy < s.rect.y0 + s.h) ? gy - s.rect.y0 : -1;

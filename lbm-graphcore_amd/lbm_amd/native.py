@@ -24,6 +24,7 @@ LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
 TRANSPORT_LOCAL, TRANSPORT_RCCL = 0, 1
 KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4 = 0, 1, 2
+FLAG_FORCE_EXCHANGE = 1
 
 # every symbol include/lbm_hip.h declares
 EXPORTED = [
@@ -67,6 +68,7 @@ class Config(ctypes.Structure):
         ("rccl_unique_id", ctypes.POINTER(ctypes.c_uint8)),
         ("kernel", ctypes.c_int32),
         ("graph_steps", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
     ]
 
 
@@ -166,7 +168,7 @@ class Engine:
     def __init__(self, params, obstacles: np.ndarray, num_gpus: int = 1, *, parts: int | None = None,
                  grid=(0, 0), transport: int = TRANSPORT_LOCAL, rank: int = 0, world: int = 1,
                  devices=None, unique_id: bytes | None = None, kernel: int = KERNEL_AUTO,
-                 graph_steps: int = 0):
+                 graph_steps: int = 0, flags: int = 0):
         self._L = load_library()
         self.params = Params(int(params.nx), int(params.ny), int(params.max_iters), int(params.reynolds_dim),
                              float(params.density), float(params.accel), float(params.omega))
@@ -188,6 +190,7 @@ class Engine:
             cfg.rccl_unique_id = self._uid
         cfg.kernel = kernel
         cfg.graph_steps = graph_steps
+        cfg.flags = flags
         rc = self._L.lbm_create_ex(ctypes.byref(self.params), obst.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
                                    ctypes.byref(cfg), ctypes.byref(self._h))
         if rc != LBM_OK:

@@ -212,3 +212,20 @@ def test_abi_errors(gpu_lib):
     with pytest.raises(gpu_lib.LbmError) as ei:
         gpu_lib.Engine(p, obst, parts=3)  # no partitionForIpus rule for 3 without an explicit grid
     assert ei.value.code == gpu_lib.LBM_E_INVALID
+
+
+@pytest.mark.parametrize("transport,parts,grid", [("local", 1, (1, 1)), ("rccl", 1, (1, 1)), ("local", 2, (1, 2)),
+                                                  ("local", 4, (2, 2))])
+def test_forced_exchange_bitwise(gpu_lib, transport, parts, grid):
+    """Every periodic wrap goes through the transport (self send/recv): the full
+    boundary/exchange/unpack/interior schedule -- with real RCCL p2p calls in
+    the rccl case -- on one GPU, bitwise vs the oracle."""
+    p, obst = load_problem("128x256", iters=19)
+    cells0 = lio.init_cells(p)
+    ref, ref_av = oracle.run(p, obst, 19, cells0)
+    kw = dict(parts=parts, grid=grid, devices=[0], flags=gpu_lib.FLAG_FORCE_EXCHANGE)
+    if transport == "rccl":
+        kw.update(transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1, unique_id=gpu_lib.rccl_unique_id())
+    cells, av, _ = gpu_run(gpu_lib, p, obst, cells0, 19, **kw)
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
