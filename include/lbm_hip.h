@@ -54,7 +54,11 @@ typedef struct lbm_params {
 } lbm_params;
 
 enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
-enum { LBM_KERNEL_AUTO = 0, LBM_KERNEL_SCALAR = 1, LBM_KERNEL_VEC4 = 2 };
+/* Step kernels: AUTO picks VEC4 for the one-step launches when widths allow;
+ * STEP2 (reported by lbm_kernel_in_use) = fused two-step launches, the
+ * default whenever every sub-domain is at least 2x2 (LBM_FLAG_ONE_STEP
+ * turns it off). */
+enum { LBM_KERNEL_AUTO = 0, LBM_KERNEL_SCALAR = 1, LBM_KERNEL_VEC4 = 2, LBM_KERNEL_STEP2 = 3 };
 
 /*
  * Placement of the 2-D block decomposition.
@@ -90,6 +94,8 @@ typedef struct lbm_config {
  * too (send to / receive from itself) instead of writing the ghost ring
  * in-kernel.  Lets one GPU exercise the full exchange path, RCCL included. */
 #define LBM_FLAG_FORCE_EXCHANGE 1
+/* One time step per launch (no fused two-step kernel). */
+#define LBM_FLAG_ONE_STEP 2
 
 typedef struct lbm_handle lbm_handle;
 
@@ -183,7 +189,7 @@ int64_t lbm_total_free_cells(lbm_handle *h);
 /* Local sub-domain rectangles of this handle (LOCAL: all; RCCL: this rank's). */
 int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *n_out);
 
-/* Which step kernel the handle uses (LBM_KERNEL_SCALAR or LBM_KERNEL_VEC4). */
+/* Which step kernel the handle uses (LBM_KERNEL_STEP2, _VEC4 or _SCALAR). */
 int32_t lbm_kernel_in_use(lbm_handle *h);
 
 const char *lbm_last_error(lbm_handle *h);

@@ -17,6 +17,10 @@
 //     an unpack kernel.
 //   * Multi-sub-domain step: boundary strip kernel -> exchange on the comm
 //     stream, overlapped with the interior kernel on the compute stream.
+//   * Two-step mode (default): each launch advances two time steps through
+//     LDS (lbm_step2.hip) and the halo is two cells wide with all nine
+//     populations (W2); an odd remaining step runs the one-step kernel (W1
+//     halo) and then refreshes the W2 ring.
 //   * The per-step |u| sums stay on the device (block partials folded by the
 //     next step's kernel); ranks combine them once, in rank order, on store.
 
@@ -36,12 +40,12 @@
 #include "lbm_layout.hpp"
 
 namespace lbm {
-hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, int flags, int min_waves,
-                       hipStream_t s);
-hipError_t launch_finalize(const float *partials, int n, float *av_local, int *ctl, hipStream_t s);
+hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hipStream_t s);
+hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t s);
+hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
-hipError_t launch_init_equilibrium(float *f, long long rows, int rf, int pitch, long long P, float c0, float c1,
+hipError_t launch_init_equilibrium(float *base, long long rows, int rf, int pitch, long long P, float c0, float c1,
                                    float c2, hipStream_t s);
 hipError_t launch_aos_to_soa(const float *aos, float *f, long long P, int pitch, int w, int h, hipStream_t s);
 hipError_t launch_soa_to_aos(const float *f, float *aos, long long P, int pitch, int w, int h, hipStream_t s);
@@ -120,35 +124,31 @@ int partition(int nx, int ny, int parts, int grid_rows, int grid_cols, int &R, i
 struct Sub {
     int id = 0, row = 0, col = 0, dev = 0;
     lbm_rect rect{};
-    int w = 0, h = 0, pitch = 0;
+    int w = 0, h = 0, pitch = 0, rf = 0;
     long long plane = 0;
-    long long lattice_floats = 0;
-    float *f[2] = {nullptr, nullptr};
-    uint8_t *obst = nullptr;
-    float *halo_mem = nullptr;  // all send + recv buffers
+    long long lattice_floats = 0, origin_off = 0;
+    float *f[2] = {nullptr, nullptr};   // allocations
+    float *o[2] = {nullptr, nullptr};   // origins: cell (0,0), plane 0
+    uint8_t *obst = nullptr;            // [h][w]
+    uint8_t *obst_g = nullptr;          // [(h+2)][(w+2)], periodic / neighbour images in the ring
+    float *halo_mem = nullptr;          // all send + recv buffers
     float *send[8] = {};
     float *recv[8] = {};
-    int nb[8] = {};             // neighbour sub id / rank per direction
+    int nb[8] = {};                     // neighbour sub id / rank per direction
     bool remote[8] = {};
     float *partials[2] = {nullptr, nullptr};
-    int n_int_blocks = 0, n_bnd_blocks = 0;
+    int n1_int = 0, n1_bnd = 0;         // one-step launch block counts
+    int n2_int = 0, n2_bnd = 0;         // two-step launch block counts
     float *av_local = nullptr;
     int av_cap = 0;
     int *ctl = nullptr;
     int accel_row = -1;
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     hipEvent_t ev_b = nullptr, ev_u = nullptr, ev_end = nullptr;
-    StepArgs args_int[2]{}, args_bnd[2]{};  // per parity
-    HaloArgs unpack[2]{};                   // per parity (lattice written by that step)
+    StepArgs a1_int[2]{}, a1_bnd[2]{};      // per parity (parity = lattice read)
+    Step2Args a2_int[2]{}, a2_bnd[2]{};
     int cur = 0;                            // lattice holding the current state
-    bool any_remote() const {
-        for (bool r : remote)
-            if (r) return true;
-        return false;
-    }
 };
-
-int edge_len(int d, int w, int h) { return d < 4 ? ((d & 1) ? w : h) : 1; }
 
 }  // namespace
 
@@ -158,14 +158,14 @@ struct lbm_handle {
     int transport = LBM_TRANSPORT_LOCAL;
     int rank = 0, world = 1;
     bool vec4 = true;
-    int graph_steps = 8;  // default: replay 16-step graphs on the single-domain path
-    // hipGraph of 2*graph_steps single-sub-domain steps, one per starting parity
+    bool two_step = true;    // fused two-step launches (W2 halo)
+    bool force_exchange = false;
+    int graph_steps = 8;     // replay graphs of 2*graph_steps launches on the single-domain path
     hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
-    // tuning knobs (environment, read at create): LBM_KFLAGS (bit0 nt stores,
-    // bit1 nt loads), LBM_MIN_WAVES, LBM_MAX_BLOCKS, LBM_LAYOUT (planar|rows)
-    // defaults chosen by tools/ab_bench.py on MI355X (profiles/r01/ab_*.log):
-    // plane-ordered kernel, row-interleaved f[y][k][x], one tile per block
-    int kflags = 4, kwaves = 1, max_blocks_cfg = 1 << 30;
+    // Tuning knobs (environment, read at create): LBM_TWO_STEP, LBM_MAX_BLOCKS,
+    // LBM_LAYOUT (rows|planar), LBM_GRAPH_STEPS, LBM_FORCE_EXCHANGE.  Defaults
+    // chosen with tools/ab_bench.py on MI355X (profiles/r01/ab_*.log).
+    int max_blocks_cfg = 1 << 30;
     bool row_interleaved = true;
     std::vector<lbm_rect> all_rects;
     std::vector<Sub> subs;  // local sub-domains
@@ -176,50 +176,13 @@ struct lbm_handle {
     double last_seconds = 0.0;
     hipEvent_t t0 = nullptr, t1 = nullptr;
     std::string err;
-    bool force_exchange = false;
+
     // any direction goes through the transport (several sub-domains, or forced)
     bool multi() const { return parts > 1 || force_exchange; }
+    int halo_mode() const { return two_step ? HALO_W2 : HALO_W1; }
 
     // ------------------------------------------------------------------
     void set_device(const Sub &s) const { HIP_CHECK(hipSetDevice(s.dev)); }
-
-    EdgeDst make_dst(const Sub &s, float *lattice, int d) const {
-        EdgeDst e{};
-        if (s.remote[d]) {
-            const int len = edge_len(d, s.w, s.h);
-            for (int i = 0; i < NPLANES[d]; ++i) e.p[i] = s.send[d] + (long long)i * len;
-            e.ps = 1;
-            return e;
-        }
-        // own ghost ring on the opposite side
-        const int g = OPP_DIR[d];
-        int xg = 0, yg = 0;
-        switch (g) {
-            case DE: xg = s.w; break;
-            case DW: xg = -1; break;
-            case DN: yg = s.h; break;
-            case DS: yg = -1; break;
-            case DNE: xg = s.w; yg = s.h; break;
-            case DNW: xg = -1; yg = s.h; break;
-            case DSW: xg = -1; yg = -1; break;
-            case DSE: xg = s.w; yg = -1; break;
-        }
-        long long base;
-        if (g == DE || g == DW) {  // column, position = y
-            base = 1LL * s.pitch + XOFF + xg;
-            e.ps = s.pitch;
-        } else if (g == DN || g == DS) {  // row, position = x
-            base = (long long)(yg + 1) * s.pitch + XOFF;
-            e.ps = 1;
-        } else {
-            base = (long long)(yg + 1) * s.pitch + XOFF + xg;
-            e.ps = 1;
-        }
-        for (int i = 0; i < NPLANES[d]; ++i) e.p[i] = lattice + PLANES[d][i] * s.plane + base;
-        return e;
-    }
-
-    int max_blocks() const { return max_blocks_cfg; }
 
     static int env_int(const char *name, int dflt) {
         const char *v = getenv(name);
@@ -227,111 +190,240 @@ struct lbm_handle {
     }
 
     void read_tuning() {
-        kflags = env_int("LBM_KFLAGS", kflags);
-        kwaves = env_int("LBM_MIN_WAVES", kwaves);
         max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
         graph_steps = std::max(0, env_int("LBM_GRAPH_STEPS", graph_steps));
+        two_step = env_int("LBM_TWO_STEP", two_step ? 1 : 0) != 0;
         const char *l = getenv("LBM_LAYOUT");
         if (l && *l) row_interleaved = std::string(l) != "planar";
     }
 
-    // rects: x0, y0 in cells; widths in cells (converted to work items here)
-    void fill_rects(StepArgs &a, const std::vector<Rect> &cells_rects, int &blocks) const {
-        const int vw = vec4 ? 4 : 1;
-        int tiles = 0;
-        a.nrect = (int)cells_rects.size();
-        for (int i = 0; i < MAX_RECTS; ++i) {
-            if (i < a.nrect) {
-                Rect r = cells_rects[i];
-                r.wc = r.wc / vw;
-                a.rect[i] = r;
-                a.rect_begin[i] = tiles;
-                const long long items = (long long)r.wc * r.hr;
-                tiles += (int)((items + BLOCK - 1) / BLOCK);
+    // ---- halo destinations --------------------------------------------
+    // W1: populations leaving through d -> own ghost ring (opposite side) or send[d]
+    EdgeDst make_dst1(const Sub &s, float *org, int d) const {
+        EdgeDst e{};
+        if (s.remote[d]) {
+            const int len = edge_len(d, s.w, s.h);
+            for (int i = 0; i < NPLANES[d]; ++i) e.p[i] = s.send[d] + (long long)i * len;
+            e.ps = 1;
+            return e;
+        }
+        long long base = 0;
+        switch (OPP_DIR[d]) {  // ghost side that receives them
+            case DE: base = s.w; e.ps = s.pitch; break;
+            case DW: base = -1; e.ps = s.pitch; break;
+            case DN: base = (long long)s.h * s.pitch; e.ps = 1; break;
+            case DS: base = -(long long)s.pitch; e.ps = 1; break;
+            case DNE: base = (long long)s.h * s.pitch + s.w; e.ps = 1; break;
+            case DNW: base = (long long)s.h * s.pitch - 1; e.ps = 1; break;
+            case DSW: base = -(long long)s.pitch - 1; e.ps = 1; break;
+            case DSE: base = -(long long)s.pitch + s.w; e.ps = 1; break;
+        }
+        for (int i = 0; i < NPLANES[d]; ++i) e.p[i] = org + PLANES[d][i] * s.plane + base;
+        return e;
+    }
+
+    // W2: the two outermost rows/columns of side d, all nine speeds, placed
+    // where the periodic image on the opposite side sits (strip coordinates
+    // (a, b) as in lbm_layout.hpp).
+    Dst2 self_dst2(const Sub &s, float *org, int d) const {
+        const long long P = s.plane, pt = s.pitch;
+        Dst2 g{};
+        g.ks = P;
+        switch (d) {
+            case DE: g.base = org - 2; g.s1 = 1; g.s2 = (int)pt; break;                 // cols w-2.. -> -2..
+            case DW: g.base = org + s.w; g.s1 = 1; g.s2 = (int)pt; break;               // cols 0..  -> w..
+            case DN: g.base = org - 2 * pt; g.s1 = (int)pt; g.s2 = 1; break;            // rows h-2.. -> -2..
+            case DS: g.base = org + (long long)s.h * pt; g.s1 = (int)pt; g.s2 = 1; break;  // rows 0.. -> h..
+            case DNE: g.base = org - 2 * pt - 2; g.s1 = (int)pt; g.s2 = 1; break;
+            case DNW: g.base = org - 2 * pt + s.w; g.s1 = (int)pt; g.s2 = 1; break;
+            case DSW: g.base = org + (long long)s.h * pt + s.w; g.s1 = (int)pt; g.s2 = 1; break;
+            case DSE: g.base = org + (long long)s.h * pt - 2; g.s1 = (int)pt; g.s2 = 1; break;
+        }
+        return g;
+    }
+
+    Dst2 make_dst2(const Sub &s, float *org, int d) const {
+        if (!s.remote[d]) return self_dst2(s, org, d);
+        Dst2 g{};
+        g.base = s.send[d];
+        if (d < 4) {  // [9][2][len]
+            const int len = edge_len(d, s.w, s.h);
+            g.ks = 2LL * len;
+            g.s1 = len;
+            g.s2 = 1;
+        } else {      // [9][2][2]
+            g.ks = 4;
+            g.s1 = 2;
+            g.s2 = 1;
+        }
+        return g;
+    }
+
+    HaloArgs halo_args(const Sub &s, float *org, int mode, bool for_unpack) const {
+        HaloArgs a{};
+        a.f = org;
+        a.plane = s.plane;
+        a.pitch = s.pitch;
+        a.w = s.w;
+        a.h = s.h;
+        a.mode = mode;
+        for (int d = 0; d < 8; ++d) {
+            if (for_unpack) {
+                if (s.remote[d]) a.mask |= 1u << d;
+                a.recv[d] = s.recv[d];
+                // side d's ghost receives the neighbour's strip of direction OPP(d)
+                a.ghost2[d] = self_dst2(s, org, OPP_DIR[d]);
             } else {
-                a.rect[i] = Rect{0, 0, 1, 1};
-                a.rect_begin[i] = INT_MAX;
+                a.mask |= 1u << d;
+                a.dst[d] = make_dst1(s, org, d);
+                a.dst2[d] = make_dst2(s, org, d);
             }
         }
-        a.total = tiles;
-        blocks = std::max(1, std::min(tiles, max_blocks()));
+        return a;
+    }
+
+    // ---- work decomposition ---------------------------------------------
+    int fill_rects(Rect (&rect)[MAX_RECTS], int (&begin)[MAX_RECTS], int &nrect, const std::vector<Rect> &rs,
+                   int unit_w, bool tiles_are_items) const {
+        int tiles = 0;
+        nrect = (int)rs.size();
+        for (int i = 0; i < MAX_RECTS; ++i) {
+            if (i < nrect) {
+                Rect r = rs[i];
+                r.wc = r.wc / unit_w;
+                rect[i] = r;
+                begin[i] = tiles;
+                const long long items = (long long)r.wc * r.hr;
+                tiles += tiles_are_items ? (int)items : (int)((items + BLOCK - 1) / BLOCK);
+            } else {
+                rect[i] = Rect{0, 0, 1, 1};
+                begin[i] = INT_MAX;
+            }
+        }
+        return tiles;
+    }
+
+    // Boundary / interior split of a sub-domain in units of `ux` x `uy`
+    // cells (x units count columns, y units rows).  xs/ys: first unit index
+    // that touches the outer strip on the high side.
+    void split(const Sub &s, int nx_u, int ny_u, int xs_hi, int ys_hi, std::vector<Rect> &bnd,
+               std::vector<Rect> &inr) const {
+        const bool xdec = s.remote[DE] || s.remote[DW];
+        const bool ydec = s.remote[DN] || s.remote[DS];
+        bnd.clear();
+        inr.clear();
+        if (!xdec && !ydec) {
+            inr.push_back(Rect{0, 0, nx_u, ny_u});
+            return;
+        }
+        const int top = std::max(1, std::min(ys_hi, ny_u));
+        bnd.push_back(Rect{0, 0, nx_u, 1});
+        if (ny_u > top) bnd.push_back(Rect{0, top, nx_u, ny_u - top});
+        const int mid_h = top - 1;
+        if (mid_h <= 0) return;
+        if (xdec) {
+            const int right = std::max(1, std::min(xs_hi, nx_u));
+            bnd.push_back(Rect{0, 1, 1, mid_h});
+            if (nx_u > right) bnd.push_back(Rect{right, 1, nx_u - right, mid_h});
+            if (right > 1) inr.push_back(Rect{1, 1, right - 1, mid_h});
+        } else {
+            inr.push_back(Rect{0, 1, nx_u, mid_h});
+        }
     }
 
     void build_args(Sub &s) {
         const float w1 = p.density * p.accel / 9.f;
         const float w2 = p.density * p.accel / 36.f;
-        const bool xdec = s.remote[DE] || s.remote[DW];
-        const bool ydec = s.remote[DN] || s.remote[DS];
-        std::vector<Rect> interior, boundary;
-        if (!xdec && !ydec) {
-            interior.push_back(Rect{0, 0, s.w, s.h});
-        } else {
-            // boundary strips: rows 0 and h-1; with x decomposed also the
-            // outermost column chunk on each side
-            const int cw = vec4 ? 4 : 1;
-            boundary.push_back(Rect{0, 0, s.w, 1});
-            if (s.h > 1) boundary.push_back(Rect{0, s.h - 1, s.w, 1});
-            const int ih = s.h - 2;
-            if (xdec) {
-                if (ih > 0) {
-                    boundary.push_back(Rect{0, 1, cw, ih});
-                    if (s.w > cw) boundary.push_back(Rect{s.w - cw, 1, cw, ih});
-                    if (s.w > 2 * cw) interior.push_back(Rect{cw, 1, s.w - 2 * cw, ih});
-                }
-            } else if (ih > 0) {
-                interior.push_back(Rect{0, 1, s.w, ih});
-            }
-            if (!ydec && !xdec) interior.clear();
-        }
-        int bi = 1, bb = 0;
-        StepArgs base{};
-        base.plane = s.plane;
-        base.pitch = s.pitch;
-        base.w = s.w;
-        base.h = s.h;
-        base.obst = s.obst;
-        base.accel_row = s.accel_row;
-        base.omega = p.omega;
-        base.omo = 1 - p.omega;
-        base.w1 = w1;
-        base.w2 = w2;
-        base.ctl = s.ctl;
-        StepArgs ai = base, ab = base;
-        fill_rects(ai, interior, bi);
-        if (!boundary.empty()) fill_rects(ab, boundary, bb);
-        s.n_int_blocks = bi;
-        s.n_bnd_blocks = boundary.empty() ? 0 : bb;
-        const int np = s.n_int_blocks + s.n_bnd_blocks;
+        std::vector<Rect> bnd, inr;
+
+        // one-step launches: units = 4-cell chunks (vec4) or cells, by rows
+        const int cw = vec4 ? 4 : 1;
+        split(s, s.w / cw, s.h, (s.w - 1) / cw, s.h - 1, bnd, inr);
+        for (auto &r : bnd) r = Rect{r.x0 * cw, r.y0, r.wc * cw, r.hr};
+        for (auto &r : inr) r = Rect{r.x0 * cw, r.y0, r.wc * cw, r.hr};
+        StepArgs b1{};
+        b1.plane = s.plane;
+        b1.pitch = s.pitch;
+        b1.w = s.w;
+        b1.h = s.h;
+        b1.obst = s.obst;
+        b1.accel_row = s.accel_row;
+        b1.omega = p.omega;
+        b1.omo = 1 - p.omega;
+        b1.w1 = w1;
+        b1.w2 = w2;
+        b1.ctl = s.ctl;
+        StepArgs ai = b1, ab = b1;
+        const int ti = fill_rects(ai.rect, ai.rect_begin, ai.nrect, inr, cw, false);
+        const int tb = fill_rects(ab.rect, ab.rect_begin, ab.nrect, bnd, cw, false);
+        ai.total = ti;
+        ab.total = tb;
+        s.n1_int = std::max(1, std::min(ti, max_blocks_cfg));
+        s.n1_bnd = bnd.empty() ? 0 : std::max(1, std::min(tb, max_blocks_cfg));
+
+        // two-step launches: units = T2W x T2H tiles, one per workgroup
+        const int tx = (s.w + T2W - 1) / T2W, ty = (s.h + T2H - 1) / T2H;
+        split(s, tx, ty, (s.w - 2) / T2W, (s.h - 2) / T2H, bnd, inr);
+        Step2Args b2{};
+        b2.obst_g = s.obst_g;
+        b2.ogp = s.w + 2;
+        b2.plane = s.plane;
+        b2.pitch = s.pitch;
+        b2.w = s.w;
+        b2.h = s.h;
+        b2.gy0 = s.rect.y0;
+        b2.ny = p.ny;
+        b2.accel_g = p.ny >= 2 ? p.ny - 2 : -1;
+        b2.omega = p.omega;
+        b2.omo = 1 - p.omega;
+        b2.w1 = w1;
+        b2.w2 = w2;
+        b2.ctl = s.ctl;
+        Step2Args ci = b2, cb = b2;
+        s.n2_int = std::max(1, fill_rects(ci.rect, ci.rect_begin, ci.nrect, inr, 1, true));
+        ci.total = s.n2_int;
+        const int t2b = fill_rects(cb.rect, cb.rect_begin, cb.nrect, bnd, 1, true);
+        cb.total = t2b;
+        s.n2_bnd = bnd.empty() ? 0 : t2b;
+        if (inr.empty()) ci.total = 0;  // one idle block keeps the reduction / partials protocol
+
+        const int n1 = s.n1_int + s.n1_bnd, n2 = s.n2_int + s.n2_bnd;
+        const int st1 = (int)round_up(n1, 4), st2 = (int)round_up(n2, 4);
+        const long long cap = std::max<long long>(st1, 2LL * st2) + 64;
         for (int k = 0; k < 2; ++k) {
             if (s.partials[k]) HIP_CHECK(hipFree(s.partials[k]));
-            HIP_CHECK(hipMalloc(&s.partials[k], sizeof(float) * (size_t)round_up(np, 64)));
-            HIP_CHECK(hipMemset(s.partials[k], 0, sizeof(float) * (size_t)round_up(np, 64)));
+            HIP_CHECK(hipMalloc(&s.partials[k], sizeof(float) * (size_t)cap));
+            HIP_CHECK(hipMemset(s.partials[k], 0, sizeof(float) * (size_t)cap));
         }
         for (int par = 0; par < 2; ++par) {
-            float *fin = s.f[par], *fout = s.f[1 - par];
+            const float *fin = s.o[par];
+            float *fout = s.o[1 - par];
             for (StepArgs *a : {&ai, &ab}) {
                 a->fin = fin;
                 a->fout = fout;
-                for (int d = 0; d < 8; ++d) a->dst[d] = make_dst(s, fout, d);
+                for (int d = 0; d < 8; ++d) a->dst[d] = make_dst1(s, fout, d);
                 a->partials_prev = s.partials[1 - par];
-                a->n_prev = np;
                 a->av_local = s.av_local;
+                a->n_total = n1;
+                a->stride = st1;
             }
             ai.partials_out = s.partials[par];
-            ab.partials_out = s.partials[par] + s.n_int_blocks;
-            s.args_int[par] = ai;
-            s.args_bnd[par] = ab;
-            HaloArgs u{};
-            u.f = fout;
-            u.plane = s.plane;
-            u.pitch = s.pitch;
-            u.w = s.w;
-            u.h = s.h;
-            for (int e = 0; e < 8; ++e) {
-                if (s.remote[e]) u.mask |= 1u << e;
-                u.recv[e] = s.recv[e];
+            ab.partials_out = s.partials[par] + s.n1_int;
+            s.a1_int[par] = ai;
+            s.a1_bnd[par] = ab;
+            for (Step2Args *a : {&ci, &cb}) {
+                a->fin = fin;
+                a->fout = fout;
+                for (int d = 0; d < 8; ++d) a->dst[d] = make_dst2(s, fout, d);
+                a->partials_prev = s.partials[1 - par];
+                a->av_local = s.av_local;
+                a->n_total = n2;
+                a->stride = st2;
             }
-            s.unpack[par] = u;
+            ci.partials_out = s.partials[par];
+            cb.partials_out = s.partials[par] + s.n2_int;
+            s.a2_int[par] = ci;
+            s.a2_bnd[par] = cb;
         }
     }
 
@@ -345,8 +437,10 @@ struct lbm_handle {
             HIP_CHECK(hipMalloc(&s.av_local, sizeof(float) * (size_t)s.av_cap));
             HIP_CHECK(hipMemset(s.av_local, 0, sizeof(float) * (size_t)s.av_cap));
             for (int par = 0; par < 2; ++par) {
-                s.args_int[par].av_local = s.av_local;
-                s.args_bnd[par].av_local = s.av_local;
+                s.a1_int[par].av_local = s.av_local;
+                s.a1_bnd[par].av_local = s.av_local;
+                s.a2_int[par].av_local = s.av_local;
+                s.a2_bnd[par].av_local = s.av_local;
             }
         }
     }
@@ -354,13 +448,15 @@ struct lbm_handle {
     // ------------------------------------------------------------------
     void create(const lbm_params *prm, const uint8_t *obstacles, const lbm_config &cfg) {
         p = *prm;
-        if (p.nx <= 0 || p.ny <= 0 || p.max_iters < 0) throw lbm_failure(LBM_E_INVALID, "nx, ny must be > 0 and max_iters >= 0");
+        if (p.nx <= 0 || p.ny <= 0 || p.max_iters < 0)
+            throw lbm_failure(LBM_E_INVALID, "nx, ny must be > 0 and max_iters >= 0");
         if (!obstacles) throw lbm_failure(LBM_E_INVALID, "obstacles must not be NULL");
         parts = cfg.parts > 0 ? cfg.parts : 1;
         transport = cfg.transport;
         read_tuning();  // environment knobs first; explicit config wins
         if (cfg.graph_steps > 0) graph_steps = cfg.graph_steps;
         if (cfg.graph_steps < 0) graph_steps = 0;
+        if (cfg.flags & LBM_FLAG_ONE_STEP) two_step = false;
         force_exchange = (cfg.flags & LBM_FLAG_FORCE_EXCHANGE) != 0 || env_int("LBM_FORCE_EXCHANGE", 0) != 0;
         if (partition(p.nx, p.ny, parts, cfg.grid_rows, cfg.grid_cols, R, C, all_rects) != LBM_OK)
             throw lbm_failure(LBM_E_INVALID, "cannot partition " + std::to_string(p.nx) + "x" + std::to_string(p.ny) +
@@ -372,14 +468,16 @@ struct lbm_handle {
         free_cells = 0;
         for (long long i = 0; i < (long long)p.nx * p.ny; ++i) free_cells += obstacles[i] ? 0 : 1;
 
-        // kernel choice
+        // kernel choice: vec4 needs widths that are multiples of 4 (>= 8 when split in x)
         bool can_vec = true;
         for (auto &r : all_rects) {
             if (r.w % 4 != 0) can_vec = false;
-            if (C > 1 && r.w < 8) can_vec = false;
+            if ((C > 1 || force_exchange) && r.w < 8) can_vec = false;
+            if (r.w < 2 || r.h < 2) two_step = false;  // the W2 strips need two rows/columns
         }
         if (cfg.kernel == LBM_KERNEL_VEC4 && !can_vec)
-            throw lbm_failure(LBM_E_INVALID, "vec4 kernel needs sub-domain widths that are multiples of 4 (>= 8 when split in x)");
+            throw lbm_failure(LBM_E_INVALID,
+                              "vec4 kernel needs sub-domain widths that are multiples of 4 (>= 8 when split in x)");
         vec4 = (cfg.kernel == LBM_KERNEL_SCALAR) ? false : can_vec;
 
         std::vector<int> mine;
@@ -453,34 +551,51 @@ struct lbm_handle {
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
         set_device(s);
-        const int row_floats = (int)round_up(s.w + XOFF + 1, 64);
-        const long long rows = s.h + 2;
-        long long total_floats;
+        s.rf = (int)round_up(s.w + XOFF + GR, 64);
+        const long long rows = s.h + 2LL * GR;
         if (row_interleaved) {
-            // f[y][k][x]: the nine populations of a row are adjacent
-            s.plane = row_floats;
-            s.pitch = Q * row_floats;
-            total_floats = rows * s.pitch;
+            // f[y][k][x]: the nine populations of a lattice row are adjacent
+            s.plane = s.rf;
+            s.pitch = Q * s.rf;
+            s.lattice_floats = rows * s.pitch;
         } else {
             // f[k][y][x]: plane stride padded off a power of two so the nine
             // concurrent plane streams do not alias
-            s.pitch = row_floats;
+            s.pitch = s.rf;
             s.plane = round_up(rows * s.pitch, 1024) + 320;
-            total_floats = Q * s.plane;
+            s.lattice_floats = Q * s.plane;
         }
-        s.lattice_floats = total_floats;
+        s.origin_off = (long long)GR * s.pitch + XOFF;
         for (int k = 0; k < 2; ++k) {
-            HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)total_floats));
-            HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)total_floats));
+            HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)s.lattice_floats));
+            HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)s.lattice_floats));
+            s.o[k] = s.f[k] + s.origin_off;
         }
         HIP_CHECK(hipMalloc(&s.obst, (size_t)round_up((long long)s.w * s.h + 16, 256)));
         HIP_CHECK(hipMemcpy2D(s.obst, (size_t)s.w, obstacles + (size_t)s.rect.y0 * p.nx + s.rect.x0, (size_t)p.nx,
                               (size_t)s.w, (size_t)s.h, hipMemcpyHostToDevice));
-        // halo buffers (only for directions that cross sub-domains)
+        // ghosted obstacle map for the two-step kernel's halo cells
+        {
+            const int gw = s.w + 2, gh = s.h + 2;
+            std::vector<uint8_t> g((size_t)gw * gh);
+            for (int y = -1; y <= s.h; ++y) {
+                const int gyy = ((s.rect.y0 + y) % p.ny + p.ny) % p.ny;
+                for (int x = -1; x <= s.w; ++x) {
+                    const int gxx = ((s.rect.x0 + x) % p.nx + p.nx) % p.nx;
+                    g[(size_t)(y + 1) * gw + (x + 1)] = obstacles[(size_t)gyy * p.nx + gxx] ? 1 : 0;
+                }
+            }
+            HIP_CHECK(hipMalloc(&s.obst_g, g.size() + 256));
+            HIP_CHECK(hipMemcpy(s.obst_g, g.data(), g.size(), hipMemcpyHostToDevice));
+        }
+        // halo buffers (only for directions that cross sub-domains), sized for
+        // the larger of the two formats
         long long total = 0;
         long long off_send[8], off_recv[8];
         for (int d = 0; d < 8; ++d) {
-            const long long n = s.remote[d] ? round_up((long long)NPLANES[d] * edge_len(d, s.w, s.h), 64) : 0;
+            const long long n =
+                s.remote[d] ? round_up(std::max(msg_floats(HALO_W1, d, s.w, s.h), msg_floats(HALO_W2, d, s.w, s.h)), 64)
+                            : 0;
             off_send[d] = total;
             total += n;
             off_recv[d] = total;
@@ -510,30 +625,31 @@ struct lbm_handle {
     }
 
     // ------------------------------------------------------------------
-    // Exchange of the halo send buffers, after every sub-domain recorded
-    // ev_b on its compute stream.  Ends with the unpack into `unpack_args`
-    // and ev_u recorded on each comm stream.
-    void exchange(const HaloArgs *unpack_args_per_sub) {
+    // Exchange of the halo send buffers (format `mode`), after every
+    // sub-domain recorded ev_b on its compute stream.  `target[k]` is the
+    // lattice origin of local sub k whose ghost ring receives.  Ends with the
+    // unpack and ev_u recorded on each comm stream.
+    void exchange(int mode, const std::vector<float *> &target) {
         if (transport == LBM_TRANSPORT_RCCL) {
             Sub &s = subs[0];
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_comm, s.ev_b, 0));
             NCCL_CHECK(ncclGroupStart());
             for (int d = 0; d < 8; ++d) {
-                // send the populations leaving through d to the neighbour on
-                // side d; receive into ghost side OPP(d) from the neighbour on
-                // that side.  Both peers enumerate d in the same order, so
-                // repeated peers (extent-2 dimensions) match in order.
+                // send the halo leaving through side d to the neighbour there;
+                // receive ghost side OPP(d) from the neighbour there.  Every
+                // rank enumerates d in the same order, so repeated peers
+                // (extent-2 dimensions, or itself) match in order.
                 if (s.remote[d])
-                    NCCL_CHECK(ncclSend(s.send[d], (size_t)NPLANES[d] * edge_len(d, s.w, s.h), ncclFloat, s.nb[d],
-                                        comm, s.s_comm));
+                    NCCL_CHECK(ncclSend(s.send[d], (size_t)msg_floats(mode, d, s.w, s.h), ncclFloat, s.nb[d], comm,
+                                        s.s_comm));
                 const int e = OPP_DIR[d];
                 if (s.remote[e])
-                    NCCL_CHECK(ncclRecv(s.recv[e], (size_t)NPLANES[e] * edge_len(e, s.w, s.h), ncclFloat, s.nb[e],
-                                        comm, s.s_comm));
+                    NCCL_CHECK(ncclRecv(s.recv[e], (size_t)msg_floats(mode, e, s.w, s.h), ncclFloat, s.nb[e], comm,
+                                        s.s_comm));
             }
             NCCL_CHECK(ncclGroupEnd());
-            HIP_CHECK(launch_halo_unpack(unpack_args_per_sub[0], s.s_comm));
+            HIP_CHECK(launch_halo_unpack(halo_args(s, target[0], mode, true), s.s_comm));
             HIP_CHECK(hipEventRecord(s.ev_u, s.s_comm));
             return;
         }
@@ -546,14 +662,14 @@ struct lbm_handle {
                 Sub *src = local_sub(s.nb[e]);
                 if (!src) throw lbm_failure(LBM_E_INTERNAL, "missing local neighbour");
                 HIP_CHECK(hipStreamWaitEvent(s.s_comm, src->ev_b, 0));
-                const size_t bytes = sizeof(float) * (size_t)NPLANES[e] * edge_len(e, s.w, s.h);
+                const size_t bytes = sizeof(float) * (size_t)msg_floats(mode, e, s.w, s.h);
                 const float *from = src->send[OPP_DIR[e]];
                 if (src->dev == s.dev)
                     HIP_CHECK(hipMemcpyAsync(s.recv[e], from, bytes, hipMemcpyDeviceToDevice, s.s_comm));
                 else
                     HIP_CHECK(hipMemcpyPeerAsync(s.recv[e], s.dev, from, src->dev, bytes, s.s_comm));
             }
-            HIP_CHECK(launch_halo_unpack(unpack_args_per_sub[k], s.s_comm));
+            HIP_CHECK(launch_halo_unpack(halo_args(s, target[k], mode, true), s.s_comm));
             HIP_CHECK(hipEventRecord(s.ev_u, s.s_comm));
         }
     }
@@ -570,52 +686,52 @@ struct lbm_handle {
         }
     }
 
-    // Make every ghost cell of the current lattices consistent (after load,
-    // init or accelerate).
+    // Make every ghost cell of the current lattices consistent in the
+    // current mode's format (after load, init, accelerate, or a trailing
+    // one-step launch in two-step mode).
     void refresh_halos() {
-        std::vector<HaloArgs> unp(subs.size());
+        const int mode = halo_mode();
+        std::vector<float *> tgt(subs.size());
         for (size_t k = 0; k < subs.size(); ++k) {
             Sub &s = subs[k];
             set_device(s);
-            HaloArgs a{};
-            a.f = s.f[s.cur];
-            a.plane = s.plane;
-            a.pitch = s.pitch;
-            a.w = s.w;
-            a.h = s.h;
-            a.mask = 0xffu;
-            for (int d = 0; d < 8; ++d) a.dst[d] = make_dst(s, s.f[s.cur], d);
-            HIP_CHECK(launch_halo_pack(a, s.s_comp));
+            HIP_CHECK(launch_halo_pack(halo_args(s, s.o[s.cur], mode, false), s.s_comp));
             HIP_CHECK(hipEventRecord(s.ev_b, s.s_comp));
-            unp[k] = s.unpack[1 - s.cur];  // unpack args of the step that produced lattice `cur`
-            unp[k].f = s.f[s.cur];
+            tgt[k] = s.o[s.cur];
         }
         if (multi()) {
-            exchange(unp.data());
+            exchange(mode, tgt);
             wait_exchange();
         }
     }
 
-    void step_once() {
+    // One launch: one time step (W1) or two (W2).
+    void launch_once(bool two) {
         if (!multi()) {
             Sub &s = subs[0];
-            HIP_CHECK(launch_step(s.args_int[s.cur], s.n_int_blocks, vec4, true, kflags, kwaves, s.s_comp));
+            if (two)
+                HIP_CHECK(launch_step2(s.a2_int[s.cur], s.n2_int, true, s.s_comp));
+            else
+                HIP_CHECK(launch_step(s.a1_int[s.cur], s.n1_int, vec4, true, s.s_comp));
             s.cur ^= 1;
             return;
         }
-        std::vector<HaloArgs> unp(subs.size());
+        std::vector<float *> tgt(subs.size());
         for (size_t k = 0; k < subs.size(); ++k) {
             Sub &s = subs[k];
             set_device(s);
-            if (s.n_bnd_blocks > 0)
-                HIP_CHECK(launch_step(s.args_bnd[s.cur], s.n_bnd_blocks, vec4, false, kflags, kwaves, s.s_comp));
+            if (two && s.n2_bnd > 0) HIP_CHECK(launch_step2(s.a2_bnd[s.cur], s.n2_bnd, false, s.s_comp));
+            if (!two && s.n1_bnd > 0) HIP_CHECK(launch_step(s.a1_bnd[s.cur], s.n1_bnd, vec4, false, s.s_comp));
             HIP_CHECK(hipEventRecord(s.ev_b, s.s_comp));
-            unp[k] = s.unpack[s.cur];
+            tgt[k] = s.o[1 - s.cur];
         }
-        exchange(unp.data());
+        exchange(two ? HALO_W2 : HALO_W1, tgt);
         for (auto &s : subs) {
             set_device(s);
-            HIP_CHECK(launch_step(s.args_int[s.cur], s.n_int_blocks, vec4, true, kflags, kwaves, s.s_comp));
+            if (two)
+                HIP_CHECK(launch_step2(s.a2_int[s.cur], s.n2_int, true, s.s_comp));
+            else
+                HIP_CHECK(launch_step(s.a1_int[s.cur], s.n1_int, vec4, true, s.s_comp));
         }
         wait_exchange();
         for (auto &s : subs) s.cur ^= 1;
@@ -629,10 +745,10 @@ struct lbm_handle {
             }
     }
 
-    // Capture 2*graph_steps steps starting at parity `par` (single sub-domain):
-    // the launch-bound small grids replay them instead of paying a host
-    // launch per step.  Kernel arguments are per parity and the av index is
-    // device-side, so one graph serves every replay.
+    // Capture 2*graph_steps launches starting at parity `par` (single
+    // sub-domain, no exchange): the step loop replays them instead of paying
+    // a host launch per step.  Kernel arguments are per parity and the av
+    // index is device-side, so one graph serves every replay.
     hipGraphExec_t graph_for(int par) {
         if (graph_exec[par]) return graph_exec[par];
         Sub &s = subs[0];
@@ -641,7 +757,8 @@ struct lbm_handle {
         HIP_CHECK(hipStreamBeginCapture(s.s_comp, hipStreamCaptureModeThreadLocal));
         int cur = par;
         for (int i = 0; i < 2 * graph_steps; ++i) {
-            const hipError_t e = launch_step(s.args_int[cur], s.n_int_blocks, vec4, true, kflags, kwaves, s.s_comp);
+            const hipError_t e = two_step ? launch_step2(s.a2_int[cur], s.n2_int, true, s.s_comp)
+                                          : launch_step(s.a1_int[cur], s.n1_int, vec4, true, s.s_comp);
             if (e != hipSuccess) {
                 hipGraph_t junk = nullptr;
                 (void)hipStreamEndCapture(s.s_comp, &junk);
@@ -669,8 +786,10 @@ struct lbm_handle {
             HIP_CHECK(hipStreamSynchronize(s.s_comp));
         }
         if (multi()) sync_all();
-        const int chunk = 2 * graph_steps;
-        const bool use_graph = !multi() && graph_steps > 0 && steps >= chunk;
+        const int per_launch = two_step ? 2 : 1;
+        const int launches = steps / per_launch;
+        const int chunk = 2 * graph_steps;  // launches per graph replay (even: parity unchanged)
+        const bool use_graph = !multi() && graph_steps > 0 && launches >= chunk;
         if (use_graph) (void)graph_for(subs[0].cur);  // capture + instantiate outside the timed region
         Sub &s0 = subs[0];
         set_device(s0);
@@ -686,20 +805,24 @@ struct lbm_handle {
             for (auto &s : subs) {
                 if (s.accel_row < 0) continue;
                 set_device(s);
-                HIP_CHECK(launch_accelerate(s.f[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+                HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
             }
             refresh_halos();
         }
-        int t = 0;
+        int l = 0;
         if (use_graph) {
-            hipGraphExec_t ge = graph_for(s0.cur);  // even chunk: parity unchanged per replay
-            for (; t + chunk <= steps; t += chunk) HIP_CHECK(hipGraphLaunch(ge, s0.s_comp));
+            set_device(s0);
+            hipGraphExec_t ge = graph_for(s0.cur);
+            for (; l + chunk <= launches; l += chunk) HIP_CHECK(hipGraphLaunch(ge, s0.s_comp));
         }
-        for (; t < steps; ++t) step_once();
+        for (; l < launches; ++l) launch_once(two_step);
+        if (two_step && steps % 2) {
+            launch_once(false);  // odd remainder: one-step kernel (W1 halo) ...
+            refresh_halos();     // ... then restore the W2 ring for the next launch
+        }
         for (auto &s : subs) {
             set_device(s);
-            const int np = s.n_int_blocks + s.n_bnd_blocks;
-            HIP_CHECK(launch_finalize(s.partials[1 - s.cur], np, s.av_local, s.ctl, s.s_comp));
+            HIP_CHECK(launch_finalize(s.partials[1 - s.cur], s.av_local, s.ctl, s.s_comp));
             HIP_CHECK(hipEventRecord(s.ev_end, s.s_comp));
         }
         set_device(s0);
@@ -726,8 +849,7 @@ struct lbm_handle {
         for (auto &s : subs) {
             set_device(s);
             s.cur = 0;
-            HIP_CHECK(launch_init_equilibrium(s.f[0], s.h + 2, (int)std::min<long long>(s.pitch, s.plane), s.pitch,
-                                              s.plane, c0, c1, c2, s.s_comp));
+            HIP_CHECK(launch_init_equilibrium(s.f[0], s.h + 2LL * GR, s.rf, s.pitch, s.plane, c0, c1, c2, s.s_comp));
         }
         sync_all();
         loaded = true;
@@ -743,7 +865,7 @@ struct lbm_handle {
             HIP_CHECK(hipMemcpy2D(stage, row_bytes, aos + ((size_t)s.rect.y0 * p.nx + s.rect.x0) * Q,
                                   sizeof(float) * Q * (size_t)p.nx, row_bytes, (size_t)s.h, hipMemcpyHostToDevice));
             s.cur = 0;
-            HIP_CHECK(launch_aos_to_soa(stage, s.f[0], s.plane, s.pitch, s.w, s.h, s.s_comp));
+            HIP_CHECK(launch_aos_to_soa(stage, s.o[0], s.plane, s.pitch, s.w, s.h, s.s_comp));
             HIP_CHECK(hipStreamSynchronize(s.s_comp));
             HIP_CHECK(hipFree(stage));
         }
@@ -761,7 +883,7 @@ struct lbm_handle {
                 float *stage = nullptr;
                 const size_t row_bytes = sizeof(float) * Q * (size_t)s.w;
                 HIP_CHECK(hipMalloc(&stage, row_bytes * (size_t)s.h));
-                HIP_CHECK(launch_soa_to_aos(s.f[s.cur], stage, s.plane, s.pitch, s.w, s.h, s.s_comp));
+                HIP_CHECK(launch_soa_to_aos(s.o[s.cur], stage, s.plane, s.pitch, s.w, s.h, s.s_comp));
                 HIP_CHECK(hipStreamSynchronize(s.s_comp));
                 HIP_CHECK(hipMemcpy2D(aos + ((size_t)s.rect.y0 * p.nx + s.rect.x0) * Q, sizeof(float) * Q * (size_t)p.nx,
                                       stage, row_bytes, row_bytes, (size_t)s.h, hipMemcpyDeviceToHost));
@@ -812,6 +934,7 @@ struct lbm_handle {
                 if (s.partials[k]) (void)hipFree(s.partials[k]);
             }
             if (s.obst) (void)hipFree(s.obst);
+            if (s.obst_g) (void)hipFree(s.obst_g);
             if (s.halo_mem) (void)hipFree(s.halo_mem);
             if (s.av_local) (void)hipFree(s.av_local);
             if (s.ctl) (void)hipFree(s.ctl);
@@ -965,7 +1088,11 @@ int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *
     return LBM_OK;
 }
 
-int32_t lbm_kernel_in_use(lbm_handle *h) { return (h && h->vec4) ? LBM_KERNEL_VEC4 : LBM_KERNEL_SCALAR; }
+int32_t lbm_kernel_in_use(lbm_handle *h) {
+    if (!h) return LBM_KERNEL_SCALAR;
+    if (h->two_step) return LBM_KERNEL_STEP2;
+    return h->vec4 ? LBM_KERNEL_VEC4 : LBM_KERNEL_SCALAR;
+}
 
 const char *lbm_last_error(lbm_handle *h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 

@@ -1,12 +1,16 @@
 // lbm_layout.hpp -- device data layout and kernel argument blocks shared by
-// the HIP kernels (lbm_kernels.hip) and the engine (lbm_engine.hip).
+// the HIP kernels (lbm_kernels.hip, lbm_step2.hip) and the engine
+// (lbm_engine.hip).
 //
-// Lattice: SoA f[9][h+2][pitch] per sub-domain, one-cell ghost ring.
-//   interior cell (x, y), 0<=x<w, 0<=y<h  ->  f[k*plane + (y+1)*pitch + XOFF + x]
-//   ghost column x=-1 sits at XOFF-1, ghost column x=w at XOFF+w,
-//   ghost rows y=-1 / y=h are rows 0 / h+1.
-// XOFF = 4 keeps every interior row 16-byte aligned for float4 access
-// (pitch and plane are multiples of 64 floats).
+// Lattice (one per ping-pong side, per sub-domain of w x h cells): SoA with a
+// ghost ring GR = 2 cells wide.  Kernels address it through an ORIGIN pointer
+// o = &f[plane 0][cell (0,0)]:
+//     cell (x, y), -2 <= x < w+2, -2 <= y < h+2, speed k  ->  o[k*plane + y*pitch + x]
+// Default layout (row-interleaved): the nine planes of a lattice row are
+// adjacent, plane = rf, pitch = 9*rf, rf = roundup(w + XOFF + GR, 64); the
+// planar layout (plane = rows*rf + pad, pitch = rf) is kept for A/B.  The
+// interior row start sits XOFF = 4 floats into each plane row, so every
+// interior float4 is 16-byte aligned.
 //
 // Speeds (main/include/LatticeBoltzmannUtils.hpp:20-22):
 //   0 M, 1 E(+1,0), 2 N(0,+1), 3 W(-1,0), 4 S(0,-1),
@@ -14,9 +18,13 @@
 // Pull streaming: s_k(x,y) = f_old[k](x - cx_k, y - cy_k)   (LastChance.cpp:203-211)
 //
 // Halo directions d = 0..7 use the velocity of speed d+1: E, N, W, S, NE, NW, SW, SE.
-// The populations that leave a sub-domain through direction d are the
-// planes whose velocity has d's non-zero components (PLANES[d]); the
-// receiving neighbour stores them in its ghost region on the opposite side.
+// Two halo formats:
+//   W1 (one-step kernels): the populations that leave through side d
+//       (PLANES[d]) of the outermost cell row/column, ghost ring width 1.
+//   W2 (two-step kernel): all nine populations of the two outermost cell
+//       rows/columns (2x2 cells at corners), ghost ring width 2 -- the
+//       intermediate step of a fused two-step launch recomputes one cell of
+//       halo, which pulls from two cells out.
 #pragma once
 
 #include <cstdint>
@@ -24,9 +32,14 @@
 namespace lbm {
 
 constexpr int Q = 9;
-constexpr int XOFF = 4;
+constexpr int XOFF = 4;   // interior column 0 offset inside a plane row
+constexpr int GR = 2;     // ghost ring width (rows/columns)
 constexpr int BLOCK = 256;  // 4 wave64s
 constexpr int MAX_RECTS = 4;
+
+// fused two-step tile (cells) and its LDS intermediate
+constexpr int T2W = 64;
+constexpr int T2H = 16;
 
 enum Dir : int { DE = 0, DN = 1, DW = 2, DS = 3, DNE = 4, DNW = 5, DSW = 6, DSE = 7 };
 
@@ -34,30 +47,47 @@ enum Dir : int { DE = 0, DN = 1, DW = 2, DS = 3, DNE = 4, DNW = 5, DSW = 6, DSE 
 constexpr int DIR_X[8] = {1, 0, -1, 0, 1, -1, -1, 1};
 constexpr int DIR_Y[8] = {0, 1, 0, -1, 1, 1, -1, -1};
 constexpr int OPP_DIR[8] = {DW, DS, DE, DN, DSW, DSE, DNE, DNW};
-// populations leaving through direction d (-1 = unused slot)
+// W1: populations leaving through direction d (-1 = unused slot)
 constexpr int PLANES[8][3] = {{1, 5, 8}, {2, 5, 6}, {3, 6, 7}, {4, 7, 8},
                               {5, -1, -1}, {6, -1, -1}, {7, -1, -1}, {8, -1, -1}};
 constexpr int NPLANES[8] = {3, 3, 3, 3, 1, 1, 1, 1};
 
-// A rectangle of the sub-domain processed by one step launch.
-// x0/y0 in cells (local), wc = width in work items (chunks of VEC cells),
-// hr = rows.
+enum HaloMode : int { HALO_W1 = 1, HALO_W2 = 2 };
+
+// A rectangle of the sub-domain processed by one step launch, in work units
+// (one-step kernels: x0/y0 in cells, wc = width in lanes' chunks, hr = rows;
+//  two-step kernel: everything in tiles).
 struct Rect {
     int x0, y0, wc, hr;
 };
 
-// Where the values of one halo direction go: either this lattice's own ghost
-// ring (periodic wrap inside one sub-domain) or a contiguous send buffer.
-// Value of plane slot i at edge position p  ->  p[i][pos * ps]
+// W1 destination of one direction: value of plane slot i at edge position p
+// -> p[i][pos * ps]   (own ghost ring, or a contiguous send buffer)
 struct EdgeDst {
     float *p[3];
     int ps;
     int pad;
 };
 
+// W2 destination of one direction: value of speed k at strip coordinates
+// (a, b) -> base[k*ks + a*s1 + b*s2].  (a, b) = (strip column, row) for E/W,
+// (strip row, column) for N/S, (strip row, strip column) for corners.
+struct Dst2 {
+    float *base;
+    long long ks;
+    int s1, s2;
+};
+
+// Average-velocity bookkeeping lives in device memory (ctl):
+//   ctl[0] = steps whose block partials are pending (0, 1 or 2)
+//   ctl[1] = next av_local index
+//   ctl[2] = partials per pending step, ctl[3] = stride between steps
+// Block 0 of every reducing launch folds the pending steps in a fixed order,
+// so no host sync or extra launch is needed per step (and graphs replay it).
+
 struct StepArgs {
-    const float *fin;       // input lattice, plane 0 base
-    float *fout;            // output lattice, plane 0 base
+    const float *fin;       // input lattice origin
+    float *fout;            // output lattice origin
     const uint8_t *obst;    // uint8[h][w]
     long long plane;        // plane stride in floats
     int pitch;              // row stride in floats
@@ -71,21 +101,51 @@ struct StepArgs {
     EdgeDst dst[8];
     // average-velocity reduction
     float *partials_out;        // this launch writes partials_out[blockIdx.x]
-    const float *partials_prev; // previous step's block partials (reduced by block 0)
-    int n_prev;
+    const float *partials_prev; // previous launch's block partials (reduced by block 0)
     float *av_local;            // per-step local sums of |u|
-    int *ctl;                   // ctl[0] = previous step pending, ctl[1] = next av index
+    int *ctl;
+    int n_total, stride;        // written to ctl by the reducing launch's block 0
 };
 
-// Halo pack (edge -> dst) used after load / accelerate, and unpack
-// (recv buffers -> ghost ring) used after every exchange.
+struct Step2Args {
+    const float *fin;
+    float *fout;
+    const uint8_t *obst_g;  // ghosted obstacles, (y+1)*ogp + (x+1), -1 <= x <= w, -1 <= y <= h
+    long long plane;
+    int pitch, ogp;
+    int w, h;
+    int gy0, ny, accel_g;   // global row of local row 0, global ny, global accelerated row (-1: none)
+    float omega, omo, w1, w2;
+    int nrect, total;       // rects in tile units; total tiles
+    Rect rect[MAX_RECTS];
+    int rect_begin[MAX_RECTS];
+    Dst2 dst[8];
+    float *partials_out;        // step s of this launch: partials_out[s*stride + blockIdx.x]
+    const float *partials_prev;
+    float *av_local;
+    int *ctl;
+    int n_total, stride;
+};
+
+// Halo pack (edge -> dst) after load / accelerate, and unpack (recv -> ghost
+// ring) after every exchange; both in either format.
 struct HaloArgs {
-    float *f;               // lattice, plane 0 base
+    float *f;               // lattice origin
     long long plane;
     int pitch, w, h;
     unsigned mask;          // directions to process
-    EdgeDst dst[8];         // pack: destination per direction
+    int mode;               // HALO_W1 / HALO_W2
+    EdgeDst dst[8];         // W1 pack destinations
+    Dst2 dst2[8];           // W2 pack destinations
+    Dst2 ghost2[8];         // W2 unpack: ghost region of side e
     const float *recv[8];   // unpack: receive buffer per direction
 };
+
+// message sizes (floats)
+inline int edge_len(int d, int w, int h) { return d < 4 ? ((d & 1) ? w : h) : 1; }
+inline long long msg_floats(int mode, int d, int w, int h) {
+    return mode == HALO_W2 ? (d < 4 ? 2LL * Q * edge_len(d, w, h) : 4LL * Q)
+                           : (long long)NPLANES[d] * edge_len(d, w, h);
+}
 
 }  // namespace lbm

@@ -29,6 +29,16 @@ def sha(cells):
     return hashlib.sha256(np.ascontiguousarray(cells, dtype="<f4").tobytes()).hexdigest()
 
 
+MODES = ["scalar", "vec4", "step2"]
+
+
+def mode_kw(native, mode):
+    """Engine options selecting one step kernel."""
+    return {"scalar": dict(kernel=native.KERNEL_SCALAR, flags=native.FLAG_ONE_STEP),
+            "vec4": dict(kernel=native.KERNEL_VEC4, flags=native.FLAG_ONE_STEP),
+            "step2": dict()}[mode]
+
+
 def gpu_run(native, p, obst, cells0, steps, accelerate=True, **kw):
     with native.Engine(p, obst, **kw) as e:
         e.load_cells(cells0)
@@ -78,17 +88,17 @@ def test_periodic_streaming_gpu(gpu_lib, nx, ny):
 
 # ------------------------------------------------------ small vectors ----
 
-@pytest.mark.parametrize("kernel", ["scalar", "vec4"])
-def test_small_vectors_bitwise(gpu_lib, kernel):
-    kid = {"scalar": gpu_lib.KERNEL_SCALAR, "vec4": gpu_lib.KERNEL_VEC4}[kernel]
+@pytest.mark.parametrize("mode", MODES)
+def test_small_vectors_bitwise(gpu_lib, mode):
     ran = 0
     for name, (p, obst, cells0, after) in small_problems().items():
-        if kernel == "vec4" and p.nx % 4:
+        if mode == "vec4" and p.nx % 4:
             continue
         for n, (ref_cells, ref_av) in after.items():
-            cells, av, used = gpu_run(gpu_lib, p, obst, cells0, n, kernel=kid)
-            assert used == kernel
-            assert np.array_equal(cells, ref_cells), (name, n, kernel)
+            cells, av, used = gpu_run(gpu_lib, p, obst, cells0, n, **mode_kw(gpu_lib, mode))
+            if mode != "step2" or (p.nx >= 2 and p.ny >= 2):
+                assert used == mode, (name, used)
+            assert np.array_equal(cells, ref_cells), (name, n, mode)
             np.testing.assert_allclose(av, ref_av, rtol=1e-5, err_msg=f"{name} {n}")
             ran += 1
     assert ran > 0
@@ -96,22 +106,23 @@ def test_small_vectors_bitwise(gpu_lib, kernel):
 
 @pytest.mark.parametrize("parts,grid", [(2, (1, 2)), (2, (2, 1)), (4, (2, 2)), (8, (2, 4)), (8, (4, 2)), (3, (3, 1)),
                                         (6, (3, 2))])
-@pytest.mark.parametrize("kernel", ["scalar", "vec4"])
-def test_decomposed_loopback_bitwise(gpu_lib, parts, grid, kernel):
+@pytest.mark.parametrize("mode", MODES)
+def test_decomposed_loopback_bitwise(gpu_lib, parts, grid, mode):
     """N sub-domains on GPU 0 (device-copy halos): lattice bitwise == single domain."""
     p, obst = load_problem("128x256", iters=23)
-    kid = {"scalar": gpu_lib.KERNEL_SCALAR, "vec4": gpu_lib.KERNEL_VEC4}[kernel]
     cells0 = lio.init_cells(p)
     ref, ref_av = oracle.run(p, obst, 23, cells0)
-    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 23, parts=parts, grid=grid, devices=[0], kernel=kid)
-    assert used == kernel
+    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 23, parts=parts, grid=grid, devices=[0],
+                              **mode_kw(gpu_lib, mode))
+    assert used == mode
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
 @pytest.mark.parametrize("parts", [2, 4, 8, 16])
-def test_decomposed_small_ragged(gpu_lib, parts):
-    """Ragged sub-domains (round-robin split, widths not multiples of 4) use the scalar kernel."""
+@pytest.mark.parametrize("mode", ["scalar", "step2"])
+def test_decomposed_small_ragged(gpu_lib, parts, mode):
+    """Ragged sub-domains (round-robin split, widths not multiples of 4)."""
     p = lio.Params(37, 29, 7, 10, 0.1, 0.02, 1.7)
     obst = np.zeros((29, 37), np.uint8)
     obst[0, :] = obst[-1, :] = 1
@@ -119,8 +130,8 @@ def test_decomposed_small_ragged(gpu_lib, parts):
     rng = np.random.default_rng(parts)
     cells0 = (lio.init_cells(p) * (1 + 0.02 * rng.standard_normal((29, 37, 9)))).astype(np.float32)
     ref, ref_av = oracle.run(p, obst, 7, cells0)
-    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 7, parts=parts, devices=[0])
-    assert used == "scalar"
+    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 7, parts=parts, devices=[0], **mode_kw(gpu_lib, mode))
+    assert used == mode
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
@@ -128,12 +139,14 @@ def test_decomposed_small_ragged(gpu_lib, parts):
 # ------------------------------------------------ reference grids ----
 
 @pytest.mark.parametrize("grid", GRIDS)
-def test_reference_grid_full_run(gpu_lib, grid, tmp_path):
+@pytest.mark.parametrize("mode", ["vec4", "step2"])
+def test_reference_grid_full_run(gpu_lib, grid, mode, tmp_path):
     """Full maxIters run: final lattice bitwise == oracle (sha256), av_vels ~ oracle,
     and the reference gate (check.py, 1 %) against check/*.dat passes."""
     p, obst = load_problem(grid)
     m = oracle_manifest(grid)
-    with gpu_lib.Engine(p, obst) as e:
+    with gpu_lib.Engine(p, obst, **mode_kw(gpu_lib, mode)) as e:
+        assert e.kernel_in_use() == mode
         e.load_cells(lio.init_cells(p))
         e.run()
         cells, av = e.store()
@@ -182,7 +195,7 @@ def test_large_grid_steps_and_conservation(gpu_lib):
     cells0 = lio.init_cells(p)
     ref, ref_av = oracle.run(p, obst, 2, cells0)
     with gpu_lib.Engine(p, obst) as e:
-        assert e.kernel_in_use() == "vec4"
+        assert e.kernel_in_use() == "step2"
         e.init_equilibrium()
         e.run_steps(2, accelerate_first=True)
         cells, av = e.store(n_av=2)
@@ -216,14 +229,16 @@ def test_abi_errors(gpu_lib):
 
 @pytest.mark.parametrize("transport,parts,grid", [("local", 1, (1, 1)), ("rccl", 1, (1, 1)), ("local", 2, (1, 2)),
                                                   ("local", 4, (2, 2))])
-def test_forced_exchange_bitwise(gpu_lib, transport, parts, grid):
+@pytest.mark.parametrize("mode", ["vec4", "step2"])
+def test_forced_exchange_bitwise(gpu_lib, transport, parts, grid, mode):
     """Every periodic wrap goes through the transport (self send/recv): the full
     boundary/exchange/unpack/interior schedule -- with real RCCL p2p calls in
     the rccl case -- on one GPU, bitwise vs the oracle."""
     p, obst = load_problem("128x256", iters=19)
     cells0 = lio.init_cells(p)
     ref, ref_av = oracle.run(p, obst, 19, cells0)
-    kw = dict(parts=parts, grid=grid, devices=[0], flags=gpu_lib.FLAG_FORCE_EXCHANGE)
+    kw = dict(parts=parts, grid=grid, devices=[0], **mode_kw(gpu_lib, mode))
+    kw["flags"] = kw.get("flags", 0) | gpu_lib.FLAG_FORCE_EXCHANGE
     if transport == "rccl":
         kw.update(transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1, unique_id=gpu_lib.rccl_unique_id())
     cells, av, _ = gpu_run(gpu_lib, p, obst, cells0, 19, **kw)

@@ -2,13 +2,13 @@
 """A/B the step kernel's tuning knobs in ONE process (interleaved rounds).
 
 Each variant is a set of LBM_* environment knobs read by lbm_create_ex
-(LBM_LAYOUT, LBM_KFLAGS, LBM_MIN_WAVES, LBM_MAX_BLOCKS).  For every round,
+(LBM_LAYOUT, LBM_MAX_BLOCKS, LBM_GRAPH_STEPS, LBM_TWO_STEP, LBM_FORCE_EXCHANGE).  For every round,
 every variant creates an engine on the same synthetic problem, warms up and
 times `steps` steps with the library's device events.  Prints one JSON line
 per variant with the median / min ms per step and GB/s (72 B per update).
 
   python tools/ab_bench.py --n 8192 --steps 100 --rounds 3 \
-      --variant base: --variant rows:LBM_LAYOUT=rows --variant nt:LBM_KFLAGS=1
+      --variant base: --variant one:LBM_TWO_STEP=0 --variant planar:LBM_LAYOUT=planar
 """
 from __future__ import annotations
 
@@ -26,7 +26,7 @@ from lbm_amd import io as lio  # noqa: E402
 from lbm_amd import native  # noqa: E402
 from bench import synthetic_obstacles  # noqa: E402
 
-KNOBS = ["LBM_LAYOUT", "LBM_KFLAGS", "LBM_MIN_WAVES", "LBM_MAX_BLOCKS"]
+KNOBS = ["LBM_LAYOUT", "LBM_MAX_BLOCKS", "LBM_GRAPH_STEPS", "LBM_TWO_STEP", "LBM_FORCE_EXCHANGE"]
 
 
 def parse_variant(s: str):

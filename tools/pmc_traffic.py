@@ -10,7 +10,7 @@ plane at row/wave seams and the 4 B/lane obstacle mask, so the doubled figure
 slightly over-counts those narrow reads (upper bound).
 
   python tools/pmc_traffic.py --fetch DIR/fetch_counter_collection.csv \
-      --write DIR/write_counter_collection.csv --key 8192x8192 --cells 67108864 \
+      --write DIR/write_counter_collection.csv --key 8192x8192/step2 --cells 67108864 \
       --out profiles/traffic.json
 """
 from __future__ import annotations
