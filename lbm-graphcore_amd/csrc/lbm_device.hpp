@@ -30,8 +30,9 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return start + (b >> 3);
 }
 
-// 256-thread block sum in a fixed order (result valid in thread 0).
-__device__ __forceinline__ float block_sum(float v, float *lds) {
+// Block sum over NW waves in a fixed order (result valid in thread 0).
+template <int NW>
+__device__ __forceinline__ float block_sum_n(float v, float *lds) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -39,48 +40,60 @@ __device__ __forceinline__ float block_sum(float v, float *lds) {
     if (lane == 0) lds[wid] = v;
     __syncthreads();
     float r = 0.f;
-    if (threadIdx.x == 0) r = ((lds[0] + lds[1]) + lds[2]) + lds[3];
+    if (threadIdx.x == 0) {
+        r = lds[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) r += lds[i];
+    }
     return r;
 }
 
-// Sum n block partials in a fixed order (depends on n only): float4 loads,
-// four independent accumulators per thread so the loads overlap, then the
-// block tree.  p must be 16-byte aligned.  Result valid in thread 0.
-__device__ __forceinline__ float sum_partials(const float *p, int n, float *lds) {
+__device__ __forceinline__ float block_sum(float v, float *lds) { return block_sum_n<BLOCK / 64>(v, lds); }
+
+// Sum n block partials in a fixed order (depends on n and NT only): float4
+// loads, four independent accumulators per thread so the loads overlap, then
+// the block tree.  p must be 16-byte aligned.  Result valid in thread 0.
+template <int NT>
+__device__ __forceinline__ float sum_partials_n(const float *p, int n, float *lds) {
     const int n4 = n >> 2;
     const float4 *p4 = reinterpret_cast<const float4 *>(p);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int i = threadIdx.x;
-    for (; i + 3 * BLOCK < n4; i += 4 * BLOCK) {
-        const float4 x0 = p4[i], x1 = p4[i + BLOCK], x2 = p4[i + 2 * BLOCK], x3 = p4[i + 3 * BLOCK];
+    for (; i + 3 * NT < n4; i += 4 * NT) {
+        const float4 x0 = p4[i], x1 = p4[i + NT], x2 = p4[i + 2 * NT], x3 = p4[i + 3 * NT];
         a0 += (x0.x + x0.y) + (x0.z + x0.w);
         a1 += (x1.x + x1.y) + (x1.z + x1.w);
         a2 += (x2.x + x2.y) + (x2.z + x2.w);
         a3 += (x3.x + x3.y) + (x3.z + x3.w);
     }
-    for (; i < n4; i += BLOCK) {
+    for (; i < n4; i += NT) {
         const float4 x0 = p4[i];
         a0 += (x0.x + x0.y) + (x0.z + x0.w);
     }
-    for (int k = 4 * n4 + threadIdx.x; k < n; k += BLOCK) a1 += p[k];
-    return block_sum((a0 + a1) + (a2 + a3), lds);
+    for (int k = 4 * n4 + threadIdx.x; k < n; k += NT) a1 += p[k];
+    return block_sum_n<NT / 64>((a0 + a1) + (a2 + a3), lds);
 }
 
-// Block 0 of a reducing launch: fold every pending step of the previous
-// launch (ctl[0] steps of ctl[2] partials, ctl[3] apart) into
+// Block 0 of a reducing launch (NT threads): fold every pending step of the
+// previous launch (ctl[0] steps of ctl[2] partials, ctl[3] apart) into
 // av_local[ctl[1]...] and advance ctl[1].
-__device__ __forceinline__ void reduce_pending(int *ctl, const float *partials, float *av_local, float *lds) {
+template <int NT>
+__device__ __forceinline__ void reduce_pending_n(int *ctl, const float *partials, float *av_local, float *lds) {
     const int pending = ctl[0];
     if (pending <= 0) return;
     const int n = ctl[2], stride = ctl[3];
     const int idx = ctl[1];
     for (int s = 0; s < pending; ++s) {
-        const float v = sum_partials(partials + (long long)s * stride, n, lds);
+        const float v = sum_partials_n<NT>(partials + (long long)s * stride, n, lds);
         if (threadIdx.x == 0) av_local[idx + s] = v;
     }
     __syncthreads();
     if (threadIdx.x == 0) ctl[1] = idx + pending;
     __syncthreads();
+}
+
+__device__ __forceinline__ void reduce_pending(int *ctl, const float *partials, float *av_local, float *lds) {
+    reduce_pending_n<BLOCK>(ctl, partials, av_local, lds);
 }
 
 __device__ __forceinline__ void publish_pending(int *ctl, int steps, int n, int stride) {

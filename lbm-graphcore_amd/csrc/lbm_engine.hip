@@ -167,6 +167,8 @@ struct lbm_handle {
     // chosen with tools/ab_bench.py on MI355X (profiles/r01/ab_*.log).
     int max_blocks_cfg = 1 << 30;
     bool row_interleaved = true;
+    int tile2 = T2_64x16;    // two-step tile shape (LBM_TILE2 = index into T2_W/T2_H)
+    int xoff = 64;           // floats before interior column 0 in a plane row (LBM_XOFF): 256-B aligned rows
     std::vector<lbm_rect> all_rects;
     std::vector<Sub> subs;  // local sub-domains
     ncclComm_t comm = nullptr;
@@ -193,6 +195,8 @@ struct lbm_handle {
         max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
         graph_steps = std::max(0, env_int("LBM_GRAPH_STEPS", graph_steps));
         two_step = env_int("LBM_TWO_STEP", two_step ? 1 : 0) != 0;
+        tile2 = std::min(std::max(env_int("LBM_TILE2", tile2), 0), NUM_TILE2 - 1);
+        xoff = std::max(GR, (env_int("LBM_XOFF", xoff) + 3) / 4 * 4);
         const char *l = getenv("LBM_LAYOUT");
         if (l && *l) row_interleaved = std::string(l) != "planar";
     }
@@ -361,10 +365,12 @@ struct lbm_handle {
         s.n1_int = std::max(1, std::min(ti, max_blocks_cfg));
         s.n1_bnd = bnd.empty() ? 0 : std::max(1, std::min(tb, max_blocks_cfg));
 
-        // two-step launches: units = T2W x T2H tiles, one per workgroup
-        const int tx = (s.w + T2W - 1) / T2W, ty = (s.h + T2H - 1) / T2H;
-        split(s, tx, ty, (s.w - 2) / T2W, (s.h - 2) / T2H, bnd, inr);
+        // two-step launches: units = TW x TH tiles, one per workgroup
+        const int TW = T2_W[tile2], TH = T2_H[tile2];
+        const int tx = (s.w + TW - 1) / TW, ty = (s.h + TH - 1) / TH;
+        split(s, tx, ty, (s.w - 2) / TW, (s.h - 2) / TH, bnd, inr);
         Step2Args b2{};
+        b2.tile = tile2;
         b2.obst_g = s.obst_g;
         b2.ogp = s.w + 2;
         b2.plane = s.plane;
@@ -551,7 +557,7 @@ struct lbm_handle {
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
         set_device(s);
-        s.rf = (int)round_up(s.w + XOFF + GR, 64);
+        s.rf = (int)round_up(s.w + xoff + GR, 64);
         const long long rows = s.h + 2LL * GR;
         if (row_interleaved) {
             // f[y][k][x]: the nine populations of a lattice row are adjacent
@@ -565,7 +571,7 @@ struct lbm_handle {
             s.plane = round_up(rows * s.pitch, 1024) + 320;
             s.lattice_floats = Q * s.plane;
         }
-        s.origin_off = (long long)GR * s.pitch + XOFF;
+        s.origin_off = (long long)GR * s.pitch + xoff;
         for (int k = 0; k < 2; ++k) {
             HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)s.lattice_floats));
             HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)s.lattice_floats));

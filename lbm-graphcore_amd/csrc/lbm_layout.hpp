@@ -37,9 +37,16 @@ constexpr int GR = 2;     // ghost ring width (rows/columns)
 constexpr int BLOCK = 256;  // 4 wave64s
 constexpr int MAX_RECTS = 4;
 
-// fused two-step tile (cells) and its LDS intermediate
-constexpr int T2W = 64;
-constexpr int T2H = 16;
+// fused two-step tile shapes (cells).  v1 (step2): LDS intermediate
+// 9 x (TH+2) x (TW+2) floats, 256 threads.  v2 (step2w): one wave per tile
+// row, TW = 64, planes 0/1/3 in registers, LDS 6 x (TH+2) x 66 floats.
+enum Tile2 : int {
+    T2_64x16 = 0, T2_64x8 = 1, T2_128x8 = 2, T2_32x16 = 3, T2_64x24 = 4,
+    T2V_64x16_W8 = 5, T2V_64x8_W8 = 6, T2V_64x16_W4 = 7, T2V_64x8_W4 = 8, T2V_64x32_W8 = 9
+};
+constexpr int NUM_TILE2 = 10;
+constexpr int T2_W[NUM_TILE2] = {64, 64, 128, 32, 64, 64, 64, 64, 64, 64};
+constexpr int T2_H[NUM_TILE2] = {16, 8, 8, 16, 24, 16, 8, 16, 8, 32};
 
 enum Dir : int { DE = 0, DN = 1, DW = 2, DS = 3, DNE = 4, DNW = 5, DSW = 6, DSE = 7 };
 
@@ -116,6 +123,7 @@ struct Step2Args {
     int w, h;
     int gy0, ny, accel_g;   // global row of local row 0, global ny, global accelerated row (-1: none)
     float omega, omo, w1, w2;
+    int tile;               // Tile2 shape
     int nrect, total;       // rects in tile units; total tiles
     Rect rect[MAX_RECTS];
     int rect_begin[MAX_RECTS];
