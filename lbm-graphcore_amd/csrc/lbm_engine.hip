@@ -167,7 +167,7 @@ struct lbm_handle {
     // chosen with tools/ab_bench.py on MI355X (profiles/r01/ab_*.log).
     int max_blocks_cfg = 1 << 30;
     bool row_interleaved = true;
-    int tile2 = T2_64x16;    // two-step tile shape (LBM_TILE2 = index into T2_W/T2_H)
+    int tile2 = -1;          // two-step tile shape (LBM_TILE2 = index into T2_W/T2_H); -1 = by size
     int xoff = 64;           // floats before interior column 0 in a plane row (LBM_XOFF): 256-B aligned rows
     std::vector<lbm_rect> all_rects;
     std::vector<Sub> subs;  // local sub-domains
@@ -195,7 +195,7 @@ struct lbm_handle {
         max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
         graph_steps = std::max(0, env_int("LBM_GRAPH_STEPS", graph_steps));
         two_step = env_int("LBM_TWO_STEP", two_step ? 1 : 0) != 0;
-        tile2 = std::min(std::max(env_int("LBM_TILE2", tile2), 0), NUM_TILE2 - 1);
+        tile2 = std::min(std::max(env_int("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
         xoff = std::max(GR, (env_int("LBM_XOFF", xoff) + 3) / 4 * 4);
         const char *l = getenv("LBM_LAYOUT");
         if (l && *l) row_interleaved = std::string(l) != "planar";
@@ -365,7 +365,11 @@ struct lbm_handle {
         s.n1_int = std::max(1, std::min(ti, max_blocks_cfg));
         s.n1_bnd = bnd.empty() ? 0 : std::max(1, std::min(tb, max_blocks_cfg));
 
-        // two-step launches: units = TW x TH tiles, one per workgroup
+        // two-step launches: units = TW x TH tiles, one per workgroup.  Tile
+        // by size (tools/ab_bench.py, profiles/r01/ab_step2_tiles.log): the
+        // wave-per-row v2 kernel wins while the lattice pair lives in the
+        // Infinity Cache, the 64x8 v1 kernel once it streams from HBM.
+        if (tile2 < 0) tile2 = ((long long)s.w * s.h <= (2LL << 20)) ? T2V_64x8_W8 : T2_64x8;
         const int TW = T2_W[tile2], TH = T2_H[tile2];
         const int tx = (s.w + TW - 1) / TW, ty = (s.h + TH - 1) / TH;
         split(s, tx, ty, (s.w - 2) / TW, (s.h - 2) / TH, bnd, inr);

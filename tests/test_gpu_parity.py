@@ -244,3 +244,28 @@ def test_forced_exchange_bitwise(gpu_lib, transport, parts, grid, mode):
     cells, av, _ = gpu_run(gpu_lib, p, obst, cells0, 19, **kw)
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.parametrize("tile", list(range(10)))
+def test_step2_tile_variants_bitwise(gpu_lib, tile, monkeypatch):
+    """Every fused two-step tile shape (v1 LDS-only and v2 wave-per-row) is
+    bitwise identical to the oracle: whole domain, 4-way loop-back, ragged."""
+    monkeypatch.setenv("LBM_TILE2", str(tile))
+    p, obst = load_problem("128x256", iters=11)
+    cells0 = lio.init_cells(p)
+    ref, ref_av = oracle.run(p, obst, 11, cells0)
+    for kw in (dict(), dict(parts=4, grid=(2, 2), devices=[0])):
+        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 11, **kw)
+        assert used == "step2"
+        assert np.array_equal(cells, ref), kw
+        np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+    q = lio.Params(70, 37, 6, 10, 0.1, 0.02, 1.7)
+    ob = np.zeros((37, 70), np.uint8)
+    ob[0, :] = ob[:, 0] = 1
+    ob[9:30, 23] = 1
+    rng = np.random.default_rng(tile)
+    c0 = (lio.init_cells(q) * (1 + 0.02 * rng.standard_normal((37, 70, 9)))).astype(np.float32)
+    r2, r2av = oracle.run(q, ob, 6, c0)
+    cells, av, _ = gpu_run(gpu_lib, q, ob, c0, 6, parts=4, devices=[0])
+    assert np.array_equal(cells, r2)
+    np.testing.assert_allclose(av, r2av, rtol=1e-5)
