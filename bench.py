@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark of the D2Q9-BGK hot path (BASELINE.json metric: MLUPS, fp32).
 
-  python bench.py [--gpus N --steps K --warmup W] [--tile 8192x8192] [--kernel auto|step2|vec4|scalar]
+  python bench.py [--gpus N --steps K --warmup W] [--tile 8192x8192]
+                  [--kernel auto|stream|step2|vec4|scalar] [--spl S]
 
 One "step" = one fused lattice update of every cell (pull-stream, rebound /
 BGK collision, folded acceleration, |u| reduction, halo exchange).
@@ -114,12 +115,12 @@ def cpu_baseline() -> dict | None:
                           f"{secs:.2f} s, 1 thread"}
 
 
-def aux_1024(kernel: int, flags: int) -> dict:
+def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
     """BASELINE config 2: the reference 1024x1024 problem, all 20 000 steps, 1 GPU."""
     gold = ROOT / "tests" / "golden" / "params"
     p = lio.Params.from_file(str(gold / "input_1024x1024.params"))
     obst = lio.read_obstacles(p.nx, p.ny, str(gold / "obstacles_1024x1024.dat"))
-    with native.Engine(p, obst, devices=[0], kernel=kernel, flags=flags) as e:
+    with native.Engine(p, obst, devices=[0], kernel=kernel, flags=flags, steps_per_launch=spl) as e:
         e.load_cells(lio.init_cells(p))
         e.run()                      # first run: warm-up + results
         _, av = e.store()
@@ -138,8 +139,10 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--tile", default="8192x8192", help="cells per GPU, NXxNY")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "step2", "vec4", "scalar"],
-                    help="auto/step2: fused two-step kernel; vec4/scalar: one step per launch")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "step2", "vec4", "scalar"],
+                    help="stream: fused S-step register-streaming kernel; step2: fused two-step LDS kernel; "
+                         "vec4/scalar: one step per launch; auto: the library's choice")
+    ap.add_argument("--spl", type=int, default=0, help="stream: time steps per launch (2..4; 0 = library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true")
     args = ap.parse_args()
@@ -150,8 +153,8 @@ def main() -> int:
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     n = world
-    kernel = {"auto": native.KERNEL_AUTO, "step2": native.KERNEL_AUTO, "scalar": native.KERNEL_SCALAR,
-              "vec4": native.KERNEL_VEC4}[args.kernel]
+    kernel = {"auto": native.KERNEL_AUTO, "stream": native.KERNEL_STREAM, "step2": native.KERNEL_STEP2,
+              "scalar": native.KERNEL_SCALAR, "vec4": native.KERNEL_VEC4}[args.kernel]
     kflags = native.FLAG_ONE_STEP if args.kernel in ("vec4", "scalar") else 0
 
     import torch
@@ -175,7 +178,8 @@ def main() -> int:
         uid = box[0]
     eng = native.Engine(p, obst, parts=n, grid=(R, C),
                         transport=native.TRANSPORT_RCCL if dist_on else native.TRANSPORT_LOCAL,
-                        rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel, flags=kflags)
+                        rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel, flags=kflags,
+                        steps_per_launch=args.spl)
     eng.init_equilibrium()
     if args.warmup > 0:
         eng.run_steps(args.warmup, accelerate_first=True)
@@ -199,18 +203,18 @@ def main() -> int:
     _, av = eng.store(cells=False, n_av=args.steps)
     finite = bool(np.all(np.isfinite(av)))
     kernel_used = eng.kernel_in_use()
+    steps_per_launch = eng.steps_per_launch()
     eng.close()
 
     total_cells = nx * ny
     value = total_cells * args.steps / elapsed / 1e6
-    # the fused two-step kernel advances two time steps per launch and moves
-    # the lattice through HBM once: 72 B per cell per launch either way
-    steps_per_launch = 2 if kernel_used == "step2" else 1
+    # a fused launch advances steps_per_launch time steps and moves the
+    # lattice through HBM once: 72 algorithmic bytes per cell per launch
     launches = max(args.steps // steps_per_launch, 1)
     per_launch_s = dev_secs / launches
     cells_per_gpu = tnx * tny
     achieved = BYTES_PER_UPDATE * cells_per_gpu / per_launch_s / 1e9
-    wl_key = f"{tnx}x{tny}/{kernel_used}"
+    wl_key = f"{tnx}x{tny}/{kernel_used}" + (str(steps_per_launch) if kernel_used == "stream" else "")
     traffic = load_traffic(wl_key)
 
     out = {
@@ -240,7 +244,7 @@ def main() -> int:
     if rank == 0 and n == 1:
         if not args.no_aux:
             try:
-                out["aux"] = {"config2_1024x1024": aux_1024(kernel, kflags)}
+                out["aux"] = {"config2_1024x1024": aux_1024(kernel, kflags, args.spl)}
             except Exception as exc:
                 out["aux"] = {"config2_1024x1024": {"error": str(exc)}}
         if not args.no_cpu_baseline:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LBM_ABI_VERSION 1
+#define LBM_ABI_VERSION 2
 
 enum {
     LBM_OK = 0,
@@ -54,11 +54,13 @@ typedef struct lbm_params {
 } lbm_params;
 
 enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
-/* Step kernels: AUTO picks VEC4 for the one-step launches when widths allow;
- * STEP2 (reported by lbm_kernel_in_use) = fused two-step launches, the
- * default whenever every sub-domain is at least 2x2 (LBM_FLAG_ONE_STEP
- * turns it off). */
-enum { LBM_KERNEL_AUTO = 0, LBM_KERNEL_SCALAR = 1, LBM_KERNEL_VEC4 = 2, LBM_KERNEL_STEP2 = 3 };
+/* Step kernels.  SCALAR / VEC4: one time step per launch (VEC4 needs widths
+ * that are multiples of 4).  STEP2: fused two-step launches through LDS.
+ * STREAM: fused S-step launches (S = steps_per_launch, 2..4) streaming rows
+ * through registers.  AUTO picks the fastest kernel the sub-domain sizes
+ * allow; lbm_kernel_in_use reports the choice.  LBM_FLAG_ONE_STEP forces one
+ * step per launch. */
+enum { LBM_KERNEL_AUTO = 0, LBM_KERNEL_SCALAR = 1, LBM_KERNEL_VEC4 = 2, LBM_KERNEL_STEP2 = 3, LBM_KERNEL_STREAM = 4 };
 
 /*
  * Placement of the 2-D block decomposition.
@@ -88,6 +90,7 @@ typedef struct lbm_config {
     int32_t graph_steps;    /* >0: replay the step loop as hipGraphs of 2*graph_steps steps
                                (single sub-domain without exchange); <0: off; 0: library default */
     int32_t flags;          /* LBM_FLAG_* */
+    int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..4); 0 = library default */
 } lbm_config;
 
 /* Route the periodic wrap of undecomposed dimensions through the transport
@@ -189,8 +192,10 @@ int64_t lbm_total_free_cells(lbm_handle *h);
 /* Local sub-domain rectangles of this handle (LOCAL: all; RCCL: this rank's). */
 int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *n_out);
 
-/* Which step kernel the handle uses (LBM_KERNEL_STEP2, _VEC4 or _SCALAR). */
+/* Which step kernel the handle uses (LBM_KERNEL_STREAM, _STEP2, _VEC4 or
+ * _SCALAR), and how many time steps one of its launches advances. */
 int32_t lbm_kernel_in_use(lbm_handle *h);
+int32_t lbm_steps_per_launch(lbm_handle *h);
 
 const char *lbm_last_error(lbm_handle *h);
 

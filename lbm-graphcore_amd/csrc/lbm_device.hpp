@@ -102,6 +102,14 @@ __device__ __forceinline__ void publish_pending(int *ctl, int steps, int n, int 
     ctl[3] = stride;
 }
 
+// Store the nine populations of one cell at strip coordinates (sa, sb) of a
+// wide-halo destination (own ghost ring or send buffer, lbm_layout.hpp Dst2).
+__device__ __forceinline__ void store2(const Dst2 &d, int sa, int sb, const float (&o)[Q]) {
+    float *p = d.base + (long long)sa * d.s1 + (long long)sb * d.s2;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) p[k * d.ks] = o[k];
+}
+
 // ---- per-cell physics -----------------------------------------------------
 
 struct Macro {

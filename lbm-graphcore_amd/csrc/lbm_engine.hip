@@ -17,10 +17,11 @@
 //     an unpack kernel.
 //   * Multi-sub-domain step: boundary strip kernel -> exchange on the comm
 //     stream, overlapped with the interior kernel on the compute stream.
-//   * Two-step mode (default): each launch advances two time steps through
-//     LDS (lbm_step2.hip) and the halo is two cells wide with all nine
-//     populations (W2); an odd remaining step runs the one-step kernel (W1
-//     halo) and then refreshes the W2 ring.
+//   * Fused mode (default): each launch advances spl time steps -- the
+//     register-streaming kernel (lbm_stream.hip, spl = 2..4) or the LDS
+//     two-step kernel (lbm_step2.hip, spl = 2) -- and the halo is spl cells
+//     wide with all nine populations (WG); remaining steps (steps % spl) run
+//     the one-step kernel (W1 halo) and then refresh the WG ring.
 //   * The per-step |u| sums stay on the device (block partials folded by the
 //     next step's kernel); ranks combine them once, in rank order, on store.
 
@@ -42,6 +43,8 @@
 namespace lbm {
 hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hipStream_t s);
 hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t s);
+hipError_t launch_stream(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
+hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
@@ -130,7 +133,7 @@ struct Sub {
     float *f[2] = {nullptr, nullptr};   // allocations
     float *o[2] = {nullptr, nullptr};   // origins: cell (0,0), plane 0
     uint8_t *obst = nullptr;            // [h][w]
-    uint8_t *obst_g = nullptr;          // [(h+2)][(w+2)], periodic / neighbour images in the ring
+    uint8_t *obst_g = nullptr;          // [(h+2og)][(w+2og)], periodic / neighbour images in the ring
     float *halo_mem = nullptr;          // all send + recv buffers
     float *send[8] = {};
     float *recv[8] = {};
@@ -143,10 +146,16 @@ struct Sub {
     int av_cap = 0;
     int *ctl = nullptr;
     int accel_row = -1;
-    hipStream_t s_comp = nullptr, s_comm = nullptr;
+    // s_comp: interior launches and everything else; s_bnd (high priority):
+    // boundary launches of multi-sub-domain runs; s_comm: halo exchange.
+    hipStream_t s_comp = nullptr, s_comm = nullptr, s_bnd = nullptr;
     hipEvent_t ev_b = nullptr, ev_u = nullptr, ev_end = nullptr;
+    hipEvent_t ev_i = nullptr;                  // interior launch done (s_comp)
+    hipEvent_t ev_bp[2] = {nullptr, nullptr};   // boundary launch done, per parity (s_bnd)
     StepArgs a1_int[2]{}, a1_bnd[2]{};      // per parity (parity = lattice read)
     Step2Args a2_int[2]{}, a2_bnd[2]{};
+    StreamArgs a3_int[2]{}, a3_bnd[2]{};
+    int n3_int = 0, n3_bnd = 0;             // stream launch block counts
     int cur = 0;                            // lattice holding the current state
 };
 
@@ -158,7 +167,18 @@ struct lbm_handle {
     int transport = LBM_TRANSPORT_LOCAL;
     int rank = 0, world = 1;
     bool vec4 = true;
-    bool two_step = true;    // fused two-step launches (W2 halo)
+    bool fused = true;       // fused multi-step launches (WG halo)
+    bool use_stream = false; // fused kernel: register-streaming (true) or LDS two-step
+    int spl = 2;             // steps per fused launch
+    int hw = 2;              // WG halo width (= spl)
+    int gr = 2;              // ghost ring width
+    int stream_s = 4;        // LBM_STREAM_S: steps per stream launch when not configured
+    int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
+    int stream_v = 2;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32)
+    int og = 4;              // ghost width of the obstacle map
+    int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
+    bool auto_stream = false; // AUTO picks the stream kernel when sizes allow
+    bool forked = false;     // boundary stream running ahead of s_comp (multi-sub-domain launches)
     bool force_exchange = false;
     int graph_steps = 8;     // replay graphs of 2*graph_steps launches on the single-domain path
     hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
@@ -181,7 +201,7 @@ struct lbm_handle {
 
     // any direction goes through the transport (several sub-domains, or forced)
     bool multi() const { return parts > 1 || force_exchange; }
-    int halo_mode() const { return two_step ? HALO_W2 : HALO_W1; }
+    int halo_mode() const { return fused ? HALO_WG : HALO_W1; }
 
     // ------------------------------------------------------------------
     void set_device(const Sub &s) const { HIP_CHECK(hipSetDevice(s.dev)); }
@@ -194,9 +214,17 @@ struct lbm_handle {
     void read_tuning() {
         max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
         graph_steps = std::max(0, env_int("LBM_GRAPH_STEPS", graph_steps));
-        two_step = env_int("LBM_TWO_STEP", two_step ? 1 : 0) != 0;
+        fused = env_int("LBM_TWO_STEP", fused ? 1 : 0) != 0;
         tile2 = std::min(std::max(env_int("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
-        xoff = std::max(GR, (env_int("LBM_XOFF", xoff) + 3) / 4 * 4);
+        xoff = std::max(MAX_GR, (env_int("LBM_XOFF", xoff) + 3) / 4 * 4);
+        stream_s = std::min(std::max(env_int("LBM_STREAM_S", stream_s), 2), 4);
+        stream_hs = std::max(0, env_int("LBM_STREAM_HS", stream_hs));
+        stream_v = env_int("LBM_STREAM_V", stream_v) == 1 ? 1 : 2;
+        if (const char *k = getenv("LBM_KERNEL")) {
+            const std::string v(k);
+            env_kernel = v == "stream" ? LBM_KERNEL_STREAM : v == "step2" ? LBM_KERNEL_STEP2
+                       : v == "vec4" ? LBM_KERNEL_VEC4 : v == "scalar" ? LBM_KERNEL_SCALAR : -1;
+        }
         const char *l = getenv("LBM_LAYOUT");
         if (l && *l) row_interleaved = std::string(l) != "planar";
     }
@@ -226,22 +254,22 @@ struct lbm_handle {
         return e;
     }
 
-    // W2: the two outermost rows/columns of side d, all nine speeds, placed
+    // WG: the hw outermost rows/columns of side d, all nine speeds, placed
     // where the periodic image on the opposite side sits (strip coordinates
     // (a, b) as in lbm_layout.hpp).
     Dst2 self_dst2(const Sub &s, float *org, int d) const {
-        const long long P = s.plane, pt = s.pitch;
+        const long long P = s.plane, pt = s.pitch, g_ = hw;
         Dst2 g{};
         g.ks = P;
         switch (d) {
-            case DE: g.base = org - 2; g.s1 = 1; g.s2 = (int)pt; break;                 // cols w-2.. -> -2..
+            case DE: g.base = org - g_; g.s1 = 1; g.s2 = (int)pt; break;                // cols w-g.. -> -g..
             case DW: g.base = org + s.w; g.s1 = 1; g.s2 = (int)pt; break;               // cols 0..  -> w..
-            case DN: g.base = org - 2 * pt; g.s1 = (int)pt; g.s2 = 1; break;            // rows h-2.. -> -2..
+            case DN: g.base = org - g_ * pt; g.s1 = (int)pt; g.s2 = 1; break;           // rows h-g.. -> -g..
             case DS: g.base = org + (long long)s.h * pt; g.s1 = (int)pt; g.s2 = 1; break;  // rows 0.. -> h..
-            case DNE: g.base = org - 2 * pt - 2; g.s1 = (int)pt; g.s2 = 1; break;
-            case DNW: g.base = org - 2 * pt + s.w; g.s1 = (int)pt; g.s2 = 1; break;
+            case DNE: g.base = org - g_ * pt - g_; g.s1 = (int)pt; g.s2 = 1; break;
+            case DNW: g.base = org - g_ * pt + s.w; g.s1 = (int)pt; g.s2 = 1; break;
             case DSW: g.base = org + (long long)s.h * pt + s.w; g.s1 = (int)pt; g.s2 = 1; break;
-            case DSE: g.base = org + (long long)s.h * pt - 2; g.s1 = (int)pt; g.s2 = 1; break;
+            case DSE: g.base = org + (long long)s.h * pt - g_; g.s1 = (int)pt; g.s2 = 1; break;
         }
         return g;
     }
@@ -250,14 +278,14 @@ struct lbm_handle {
         if (!s.remote[d]) return self_dst2(s, org, d);
         Dst2 g{};
         g.base = s.send[d];
-        if (d < 4) {  // [9][2][len]
+        if (d < 4) {  // [9][hw][len]
             const int len = edge_len(d, s.w, s.h);
-            g.ks = 2LL * len;
+            g.ks = (long long)hw * len;
             g.s1 = len;
             g.s2 = 1;
-        } else {      // [9][2][2]
-            g.ks = 4;
-            g.s1 = 2;
+        } else {      // [9][hw][hw]
+            g.ks = (long long)hw * hw;
+            g.s1 = hw;
             g.s2 = 1;
         }
         return g;
@@ -271,6 +299,7 @@ struct lbm_handle {
         a.w = s.w;
         a.h = s.h;
         a.mode = mode;
+        a.g = hw;
         for (int d = 0; d < 8; ++d) {
             if (for_unpack) {
                 if (s.remote[d]) a.mask |= 1u << d;
@@ -375,8 +404,8 @@ struct lbm_handle {
         split(s, tx, ty, (s.w - 2) / TW, (s.h - 2) / TH, bnd, inr);
         Step2Args b2{};
         b2.tile = tile2;
-        b2.obst_g = s.obst_g;
-        b2.ogp = s.w + 2;
+        b2.ogp = s.w + 2 * og;
+        b2.obst_g = s.obst_g + (long long)(og - 1) * b2.ogp + (og - 1);  // the kernel indexes (y+1)*ogp + (x+1)
         b2.plane = s.plane;
         b2.pitch = s.pitch;
         b2.w = s.w;
@@ -397,9 +426,40 @@ struct lbm_handle {
         s.n2_bnd = bnd.empty() ? 0 : t2b;
         if (inr.empty()) ci.total = 0;  // one idle block keeps the reduction / partials protocol
 
-        const int n1 = s.n1_int + s.n1_bnd, n2 = s.n2_int + s.n2_bnd;
-        const int st1 = (int)round_up(n1, 4), st2 = (int)round_up(n2, 4);
-        const long long cap = std::max<long long>(st1, 2LL * st2) + 64;
+        // stream launches: rects in cells, units = strip x segment (one wave
+        // each).  Decomposed dimensions get boundary bands spl cells deep so
+        // the interior never reads the ghost ring.
+        StreamArgs b3{};
+        b3.obst_g = s.obst_g;
+        b3.og = og;
+        b3.ogp = s.w + 2 * og;
+        b3.plane = s.plane;
+        b3.pitch = s.pitch;
+        b3.w = s.w;
+        b3.h = s.h;
+        b3.xmax = s.rf - xoff - 1;  // last column inside the row allocation (>= w + gr + 1)
+        b3.gy0 = s.rect.y0;
+        b3.ny = p.ny;
+        b3.accel_g = p.ny >= 2 ? p.ny - 2 : -1;
+        b3.omega = p.omega;
+        b3.omo = 1 - p.omega;
+        b3.w1 = w1;
+        b3.w2 = w2;
+        b3.ctl = s.ctl;
+        StreamArgs si = b3, sb = b3;
+        s.n3_int = s.n3_bnd = 0;
+        if (use_stream) {
+            std::vector<SRect> ri, rb;
+            stream_split(s, ri, rb);
+            si.total = fill_srects(si, ri);
+            sb.total = fill_srects(sb, rb);
+            s.n3_int = std::max(1, si.total);  // one idle block keeps the reduction / partials protocol
+            s.n3_bnd = sb.total;
+        }
+
+        const int n1 = s.n1_int + s.n1_bnd, n2 = s.n2_int + s.n2_bnd, n3 = s.n3_int + s.n3_bnd;
+        const int st1 = (int)round_up(n1, 4), st2 = (int)round_up(n2, 4), st3 = (int)round_up(n3, 4);
+        const long long cap = std::max<long long>(std::max<long long>(st1, 2LL * st2), (long long)spl * st3) + 64;
         for (int k = 0; k < 2; ++k) {
             if (s.partials[k]) HIP_CHECK(hipFree(s.partials[k]));
             HIP_CHECK(hipMalloc(&s.partials[k], sizeof(float) * (size_t)cap));
@@ -434,7 +494,72 @@ struct lbm_handle {
             cb.partials_out = s.partials[par] + s.n2_int;
             s.a2_int[par] = ci;
             s.a2_bnd[par] = cb;
+            for (StreamArgs *a : {&si, &sb}) {
+                a->fin = fin;
+                a->fout = fout;
+                for (int d = 0; d < 8; ++d) a->dst[d] = make_dst2(s, fout, d);
+                a->partials_prev = s.partials[1 - par];
+                a->av_local = s.av_local;
+                a->n_total = n3;
+                a->stride = st3;
+            }
+            si.partials_out = s.partials[par];
+            sb.partials_out = s.partials[par] + s.n3_int;
+            s.a3_int[par] = si;
+            s.a3_bnd[par] = sb;
         }
+    }
+
+    // Stream-kernel work split of a sub-domain (cells).  Segment height by
+    // size: about 16 waves per CU over the interior, at least 4*spl rows so
+    // the 2*spl re-streamed rows per segment stay a small overhead.
+    void stream_split(const Sub &s, std::vector<SRect> &inr, std::vector<SRect> &bnd) const {
+        const int S = spl, b = S;
+        // owned columns per strip: 64 - 2S (one column per lane); 128 - 2S
+        // (two per lane), 2 fewer when the strip's first cell minus S is odd
+        // (float2 alignment shifts the wave one column left)
+        auto ow_of = [&](int rx) { return stream_v == 1 ? 64 - 2 * S : (((rx - S) & 1) ? 126 - 2 * S : 128 - 2 * S); };
+        const bool xdec = s.remote[DE] || s.remote[DW];
+        const bool ydec = s.remote[DN] || s.remote[DS];
+        const int y0 = ydec ? b : 0, y1 = ydec ? s.h - b : s.h;
+        const int x0 = xdec ? b : 0, x1 = xdec ? s.w - b : s.w;
+        int hs = stream_hs;
+        if (hs <= 0) {
+            const long long strips = (std::max(x1 - x0, 1) + ow_of(x0) - 1) / ow_of(x0);
+            const long long target = 4096;
+            hs = (int)std::max<long long>(4LL * S, (std::max(y1 - y0, 1) * strips + target - 1) / target);
+        }
+        auto mk = [&](int rx, int ry, int rw, int rh, int rhs) {
+            const int ow = ow_of(rx);
+            return SRect{rx, ry, rw, rh, (rw + ow - 1) / ow, std::max(1, std::min(rhs, rh)), ow};
+        };
+        inr.clear();
+        bnd.clear();
+        if (ydec) {
+            bnd.push_back(mk(0, 0, s.w, b, b));
+            bnd.push_back(mk(0, s.h - b, s.w, b, b));
+        }
+        if (xdec && y1 > y0) {
+            bnd.push_back(mk(0, y0, b, y1 - y0, hs));
+            bnd.push_back(mk(s.w - b, y0, b, y1 - y0, hs));
+        }
+        if (x1 > x0 && y1 > y0) inr.push_back(mk(x0, y0, x1 - x0, y1 - y0, hs));
+    }
+
+    int fill_srects(StreamArgs &a, const std::vector<SRect> &rs) const {
+        int units = 0;
+        a.nrect = (int)rs.size();
+        for (int i = 0; i < MAX_RECTS; ++i) {
+            if (i < a.nrect) {
+                a.rect[i] = rs[i];
+                a.rect_begin[i] = units;
+                units += rs[i].nstrip * ((rs[i].h + rs[i].hs - 1) / rs[i].hs);
+            } else {
+                a.rect[i] = SRect{0, 0, 1, 1, 1, 1, 1};
+                a.rect_begin[i] = INT_MAX;
+            }
+        }
+        return units;
     }
 
     void ensure_av(int n) {
@@ -451,6 +576,8 @@ struct lbm_handle {
                 s.a1_bnd[par].av_local = s.av_local;
                 s.a2_int[par].av_local = s.av_local;
                 s.a2_bnd[par].av_local = s.av_local;
+                s.a3_int[par].av_local = s.av_local;
+                s.a3_bnd[par].av_local = s.av_local;
             }
         }
     }
@@ -466,7 +593,7 @@ struct lbm_handle {
         read_tuning();  // environment knobs first; explicit config wins
         if (cfg.graph_steps > 0) graph_steps = cfg.graph_steps;
         if (cfg.graph_steps < 0) graph_steps = 0;
-        if (cfg.flags & LBM_FLAG_ONE_STEP) two_step = false;
+        if (cfg.flags & LBM_FLAG_ONE_STEP) fused = false;
         force_exchange = (cfg.flags & LBM_FLAG_FORCE_EXCHANGE) != 0 || env_int("LBM_FORCE_EXCHANGE", 0) != 0;
         if (partition(p.nx, p.ny, parts, cfg.grid_rows, cfg.grid_cols, R, C, all_rects) != LBM_OK)
             throw lbm_failure(LBM_E_INVALID, "cannot partition " + std::to_string(p.nx) + "x" + std::to_string(p.ny) +
@@ -483,12 +610,34 @@ struct lbm_handle {
         for (auto &r : all_rects) {
             if (r.w % 4 != 0) can_vec = false;
             if ((C > 1 || force_exchange) && r.w < 8) can_vec = false;
-            if (r.w < 2 || r.h < 2) two_step = false;  // the W2 strips need two rows/columns
+            if (r.w < 2 || r.h < 2) fused = false;  // the two-step halo strips need two rows/columns
         }
-        if (cfg.kernel == LBM_KERNEL_VEC4 && !can_vec)
+        const int kernel = (cfg.kernel == LBM_KERNEL_AUTO && env_kernel >= 0) ? env_kernel : cfg.kernel;
+        if (kernel == LBM_KERNEL_VEC4 && !can_vec)
             throw lbm_failure(LBM_E_INVALID,
                               "vec4 kernel needs sub-domain widths that are multiples of 4 (>= 8 when split in x)");
-        vec4 = (cfg.kernel == LBM_KERNEL_SCALAR) ? false : can_vec;
+        vec4 = (kernel == LBM_KERNEL_SCALAR) ? false : can_vec;
+        if (kernel == LBM_KERNEL_VEC4 || kernel == LBM_KERNEL_SCALAR) {
+            if (env_kernel >= 0 && cfg.kernel == LBM_KERNEL_AUTO) fused = false;  // LBM_KERNEL=vec4|scalar: one step per launch
+        }
+        // register-streaming kernel: S steps per launch, S-wide ghost ring;
+        // every sub-domain at least S cells (2S across a decomposed dimension)
+        const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch : stream_s;
+        if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > 4))
+            throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2..4");
+        bool can_stream = fused && S >= 2 && S <= 4;
+        for (auto &r : all_rects) {
+            const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;
+            if (r.w < mw || r.h < mh) can_stream = false;
+        }
+        if (kernel == LBM_KERNEL_STREAM && !can_stream)
+            throw lbm_failure(LBM_E_INVALID, "stream kernel needs fused launches and sub-domains of at least "
+                                             "steps_per_launch cells (twice that across a decomposed dimension)");
+        use_stream = kernel == LBM_KERNEL_STREAM || (kernel == LBM_KERNEL_AUTO && auto_stream && can_stream);
+        spl = use_stream ? S : 2;
+        hw = spl;
+        gr = std::max(2, hw);
+        og = gr + 2;  // the two-column stream kernel's strips start up to S+1 columns left of their first cell
 
         std::vector<int> mine;
         if (transport == LBM_TRANSPORT_RCCL) {
@@ -561,8 +710,10 @@ struct lbm_handle {
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
         set_device(s);
-        s.rf = (int)round_up(s.w + xoff + GR, 64);
-        const long long rows = s.h + 2LL * GR;
+        // two spare columns past the ring: a two-column stream lane reads its
+        // pair unclamped up to column w + gr
+        s.rf = (int)round_up(s.w + xoff + gr + 2, 64);
+        const long long rows = s.h + 2LL * gr;
         if (row_interleaved) {
             // f[y][k][x]: the nine populations of a lattice row are adjacent
             s.plane = s.rf;
@@ -575,7 +726,7 @@ struct lbm_handle {
             s.plane = round_up(rows * s.pitch, 1024) + 320;
             s.lattice_floats = Q * s.plane;
         }
-        s.origin_off = (long long)GR * s.pitch + xoff;
+        s.origin_off = (long long)gr * s.pitch + xoff;
         for (int k = 0; k < 2; ++k) {
             HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)s.lattice_floats));
             HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)s.lattice_floats));
@@ -584,15 +735,15 @@ struct lbm_handle {
         HIP_CHECK(hipMalloc(&s.obst, (size_t)round_up((long long)s.w * s.h + 16, 256)));
         HIP_CHECK(hipMemcpy2D(s.obst, (size_t)s.w, obstacles + (size_t)s.rect.y0 * p.nx + s.rect.x0, (size_t)p.nx,
                               (size_t)s.w, (size_t)s.h, hipMemcpyHostToDevice));
-        // ghosted obstacle map for the two-step kernel's halo cells
+        // ghosted obstacle map (ring of og cells) for the fused kernels' halo cells
         {
-            const int gw = s.w + 2, gh = s.h + 2;
+            const int gw = s.w + 2 * og, gh = s.h + 2 * og;
             std::vector<uint8_t> g((size_t)gw * gh);
-            for (int y = -1; y <= s.h; ++y) {
+            for (int y = -og; y < s.h + og; ++y) {
                 const int gyy = ((s.rect.y0 + y) % p.ny + p.ny) % p.ny;
-                for (int x = -1; x <= s.w; ++x) {
+                for (int x = -og; x < s.w + og; ++x) {
                     const int gxx = ((s.rect.x0 + x) % p.nx + p.nx) % p.nx;
-                    g[(size_t)(y + 1) * gw + (x + 1)] = obstacles[(size_t)gyy * p.nx + gxx] ? 1 : 0;
+                    g[(size_t)(y + og) * gw + (x + og)] = obstacles[(size_t)gyy * p.nx + gxx] ? 1 : 0;
                 }
             }
             HIP_CHECK(hipMalloc(&s.obst_g, g.size() + 256));
@@ -604,7 +755,7 @@ struct lbm_handle {
         long long off_send[8], off_recv[8];
         for (int d = 0; d < 8; ++d) {
             const long long n =
-                s.remote[d] ? round_up(std::max(msg_floats(HALO_W1, d, s.w, s.h), msg_floats(HALO_W2, d, s.w, s.h)), 64)
+                s.remote[d] ? round_up(std::max(msg_floats(HALO_W1, d, s.w, s.h, hw), msg_floats(HALO_WG, d, s.w, s.h, hw)), 64)
                             : 0;
             off_send[d] = total;
             total += n;
@@ -623,7 +774,12 @@ struct lbm_handle {
         HIP_CHECK(hipMemset(s.ctl, 0, 64));
         HIP_CHECK(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
+        int prio_lo = 0, prio_hi = 0;
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIP_CHECK(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, prio_hi));
         HIP_CHECK(hipEventCreateWithFlags(&s.ev_b, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&s.ev_i, hipEventDisableTiming));
+        for (auto &e : s.ev_bp) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&s.ev_u, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&s.ev_end, hipEventDisableTiming));
     }
@@ -651,11 +807,11 @@ struct lbm_handle {
                 // rank enumerates d in the same order, so repeated peers
                 // (extent-2 dimensions, or itself) match in order.
                 if (s.remote[d])
-                    NCCL_CHECK(ncclSend(s.send[d], (size_t)msg_floats(mode, d, s.w, s.h), ncclFloat, s.nb[d], comm,
+                    NCCL_CHECK(ncclSend(s.send[d], (size_t)msg_floats(mode, d, s.w, s.h, hw), ncclFloat, s.nb[d], comm,
                                         s.s_comm));
                 const int e = OPP_DIR[d];
                 if (s.remote[e])
-                    NCCL_CHECK(ncclRecv(s.recv[e], (size_t)msg_floats(mode, e, s.w, s.h), ncclFloat, s.nb[e], comm,
+                    NCCL_CHECK(ncclRecv(s.recv[e], (size_t)msg_floats(mode, e, s.w, s.h, hw), ncclFloat, s.nb[e], comm,
                                         s.s_comm));
             }
             NCCL_CHECK(ncclGroupEnd());
@@ -672,7 +828,7 @@ struct lbm_handle {
                 Sub *src = local_sub(s.nb[e]);
                 if (!src) throw lbm_failure(LBM_E_INTERNAL, "missing local neighbour");
                 HIP_CHECK(hipStreamWaitEvent(s.s_comm, src->ev_b, 0));
-                const size_t bytes = sizeof(float) * (size_t)msg_floats(mode, e, s.w, s.h);
+                const size_t bytes = sizeof(float) * (size_t)msg_floats(mode, e, s.w, s.h, hw);
                 const float *from = src->send[OPP_DIR[e]];
                 if (src->dev == s.dev)
                     HIP_CHECK(hipMemcpyAsync(s.recv[e], from, bytes, hipMemcpyDeviceToDevice, s.s_comm));
@@ -684,15 +840,19 @@ struct lbm_handle {
         }
     }
 
-    // Compute streams wait for the exchange: own ghosts unpacked, and (LOCAL)
+    // `st` waits for the last exchange: own ghosts unpacked, and (LOCAL)
     // every neighbour done reading this sub-domain's send buffers.
+    void wait_exchange_on(Sub &s, hipStream_t st) {
+        HIP_CHECK(hipStreamWaitEvent(st, s.ev_u, 0));
+        if (transport == LBM_TRANSPORT_LOCAL)
+            for (int d = 0; d < 8; ++d)
+                if (s.remote[d]) HIP_CHECK(hipStreamWaitEvent(st, local_sub(s.nb[d])->ev_u, 0));
+    }
+
     void wait_exchange() {
         for (auto &s : subs) {
             set_device(s);
-            HIP_CHECK(hipStreamWaitEvent(s.s_comp, s.ev_u, 0));
-            if (transport == LBM_TRANSPORT_LOCAL)
-                for (int d = 0; d < 8; ++d)
-                    if (s.remote[d]) HIP_CHECK(hipStreamWaitEvent(s.s_comp, local_sub(s.nb[d])->ev_u, 0));
+            wait_exchange_on(s, s.s_comp);
         }
     }
 
@@ -715,36 +875,80 @@ struct lbm_handle {
         }
     }
 
-    // One launch: one time step (W1) or two (W2).
+    // Interior (reducing) or boundary launch of sub-domain s reading parity
+    // `cur`: one fused launch (spl steps, WG halo) or one step (W1 halo).
+    hipError_t launch_part(Sub &s, int cur, bool fused_launch, bool interior, hipStream_t st) const {
+        if (fused_launch && use_stream) {
+            const int n = interior ? s.n3_int : s.n3_bnd;
+            if (n <= 0) return hipSuccess;
+            const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
+            return stream_v == 1 ? launch_stream(a, n, spl, interior, st) : launch_stream2c(a, n, spl, interior, st);
+        }
+        if (fused_launch) {
+            const int n = interior ? s.n2_int : s.n2_bnd;
+            return n > 0 ? launch_step2(interior ? s.a2_int[cur] : s.a2_bnd[cur], n, interior, st) : hipSuccess;
+        }
+        const int n = interior ? s.n1_int : s.n1_bnd;
+        return n > 0 ? launch_step(interior ? s.a1_int[cur] : s.a1_bnd[cur], n, vec4, interior, st) : hipSuccess;
+    }
+
+    // One launch: one time step (W1 halo) or spl steps (fused, WG halo).
+    //
+    // Multi-sub-domain launch t (reads lattice c = cur, writes 1-c):
+    //   B(t) boundary tiles on s_bnd, after I(t-1) (it overwrites the cells
+    //        I(t-1) read, and the partials I(t-1) reduced) and after the
+    //        exchange U(t-1) that filled c's ghost ring (LOCAL: and after
+    //        every neighbour finished copying this sub-domain's send buffers);
+    //   X(t) exchange + unpack on s_comm, after B(t) (exchange());
+    //   I(t) interior tiles on s_comp, after B(t-1) only: interior tiles
+    //        never read the ghost ring, so the exchange of launch t-1 runs
+    //        under I(t) and B(t+1) overlaps I(t+1)'s tail.
+    // join() re-serialises everything onto s_comp.
     void launch_once(bool two) {
         if (!multi()) {
             Sub &s = subs[0];
-            if (two)
-                HIP_CHECK(launch_step2(s.a2_int[s.cur], s.n2_int, true, s.s_comp));
-            else
-                HIP_CHECK(launch_step(s.a1_int[s.cur], s.n1_int, vec4, true, s.s_comp));
+            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp));
             s.cur ^= 1;
             return;
+        }
+        if (!forked) {
+            for (auto &s : subs) {
+                set_device(s);
+                HIP_CHECK(hipEventRecord(s.ev_i, s.s_comp));  // B(first) after all prior s_comp work
+            }
+            forked = true;
         }
         std::vector<float *> tgt(subs.size());
         for (size_t k = 0; k < subs.size(); ++k) {
             Sub &s = subs[k];
             set_device(s);
-            if (two && s.n2_bnd > 0) HIP_CHECK(launch_step2(s.a2_bnd[s.cur], s.n2_bnd, false, s.s_comp));
-            if (!two && s.n1_bnd > 0) HIP_CHECK(launch_step(s.a1_bnd[s.cur], s.n1_bnd, vec4, false, s.s_comp));
-            HIP_CHECK(hipEventRecord(s.ev_b, s.s_comp));
+            HIP_CHECK(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
+            wait_exchange_on(s, s.s_bnd);
+            HIP_CHECK(launch_part(s, s.cur, two, false, s.s_bnd));
+            HIP_CHECK(hipEventRecord(s.ev_b, s.s_bnd));
+            HIP_CHECK(hipEventRecord(s.ev_bp[s.cur], s.s_bnd));
             tgt[k] = s.o[1 - s.cur];
         }
-        exchange(two ? HALO_W2 : HALO_W1, tgt);
+        exchange(two ? HALO_WG : HALO_W1, tgt);
         for (auto &s : subs) {
             set_device(s);
-            if (two)
-                HIP_CHECK(launch_step2(s.a2_int[s.cur], s.n2_int, true, s.s_comp));
-            else
-                HIP_CHECK(launch_step(s.a1_int[s.cur], s.n1_int, vec4, true, s.s_comp));
+            HIP_CHECK(hipStreamWaitEvent(s.s_comp, s.ev_bp[1 - s.cur], 0));  // B(t-1)
+            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp));
+            HIP_CHECK(hipEventRecord(s.ev_i, s.s_comp));
+        }
+        for (auto &s : subs) s.cur ^= 1;
+    }
+
+    // After a run of launch_once: s_comp waits for the last boundary launch
+    // and the last exchange, so later s_comp work sees a complete state.
+    void join() {
+        if (!forked) return;
+        for (auto &s : subs) {
+            set_device(s);
+            HIP_CHECK(hipStreamWaitEvent(s.s_comp, s.ev_bp[1 - s.cur], 0));
         }
         wait_exchange();
-        for (auto &s : subs) s.cur ^= 1;
+        forked = false;
     }
 
     void drop_graphs() {
@@ -767,8 +971,7 @@ struct lbm_handle {
         HIP_CHECK(hipStreamBeginCapture(s.s_comp, hipStreamCaptureModeThreadLocal));
         int cur = par;
         for (int i = 0; i < 2 * graph_steps; ++i) {
-            const hipError_t e = two_step ? launch_step2(s.a2_int[cur], s.n2_int, true, s.s_comp)
-                                          : launch_step(s.a1_int[cur], s.n1_int, vec4, true, s.s_comp);
+            const hipError_t e = launch_part(s, cur, fused, true, s.s_comp);
             if (e != hipSuccess) {
                 hipGraph_t junk = nullptr;
                 (void)hipStreamEndCapture(s.s_comp, &junk);
@@ -796,7 +999,7 @@ struct lbm_handle {
             HIP_CHECK(hipStreamSynchronize(s.s_comp));
         }
         if (multi()) sync_all();
-        const int per_launch = two_step ? 2 : 1;
+        const int per_launch = fused ? spl : 1;
         const int launches = steps / per_launch;
         const int chunk = 2 * graph_steps;  // launches per graph replay (even: parity unchanged)
         const bool use_graph = !multi() && graph_steps > 0 && launches >= chunk;
@@ -825,11 +1028,11 @@ struct lbm_handle {
             hipGraphExec_t ge = graph_for(s0.cur);
             for (; l + chunk <= launches; l += chunk) HIP_CHECK(hipGraphLaunch(ge, s0.s_comp));
         }
-        for (; l < launches; ++l) launch_once(two_step);
-        if (two_step && steps % 2) {
-            launch_once(false);  // odd remainder: one-step kernel (W1 halo) ...
-            refresh_halos();     // ... then restore the W2 ring for the next launch
-        }
+        for (; l < launches; ++l) launch_once(fused);
+        const int rem = steps - launches * per_launch;
+        for (int i = 0; i < rem; ++i) launch_once(false);  // remainder: one-step kernel (W1 halo) ...
+        join();
+        if (rem > 0) refresh_halos();                      // ... then restore the WG ring for the next launch
         for (auto &s : subs) {
             set_device(s);
             HIP_CHECK(launch_finalize(s.partials[1 - s.cur], s.av_local, s.ctl, s.s_comp));
@@ -851,6 +1054,7 @@ struct lbm_handle {
             set_device(s);
             HIP_CHECK(hipStreamSynchronize(s.s_comp));
             HIP_CHECK(hipStreamSynchronize(s.s_comm));
+            HIP_CHECK(hipStreamSynchronize(s.s_bnd));
         }
     }
 
@@ -859,7 +1063,7 @@ struct lbm_handle {
         for (auto &s : subs) {
             set_device(s);
             s.cur = 0;
-            HIP_CHECK(launch_init_equilibrium(s.f[0], s.h + 2LL * GR, s.rf, s.pitch, s.plane, c0, c1, c2, s.s_comp));
+            HIP_CHECK(launch_init_equilibrium(s.f[0], s.h + 2LL * gr, s.rf, s.pitch, s.plane, c0, c1, c2, s.s_comp));
         }
         sync_all();
         loaded = true;
@@ -950,6 +1154,10 @@ struct lbm_handle {
             if (s.ctl) (void)hipFree(s.ctl);
             if (s.s_comp) (void)hipStreamDestroy(s.s_comp);
             if (s.s_comm) (void)hipStreamDestroy(s.s_comm);
+            if (s.s_bnd) (void)hipStreamDestroy(s.s_bnd);
+            if (s.ev_i) (void)hipEventDestroy(s.ev_i);
+            for (auto e : s.ev_bp)
+                if (e) (void)hipEventDestroy(e);
             if (s.ev_b) (void)hipEventDestroy(s.ev_b);
             if (s.ev_u) (void)hipEventDestroy(s.ev_u);
             if (s.ev_end) (void)hipEventDestroy(s.ev_end);
@@ -1100,9 +1308,11 @@ int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *
 
 int32_t lbm_kernel_in_use(lbm_handle *h) {
     if (!h) return LBM_KERNEL_SCALAR;
-    if (h->two_step) return LBM_KERNEL_STEP2;
+    if (h->fused) return h->use_stream ? LBM_KERNEL_STREAM : LBM_KERNEL_STEP2;
     return h->vec4 ? LBM_KERNEL_VEC4 : LBM_KERNEL_SCALAR;
 }
+
+int32_t lbm_steps_per_launch(lbm_handle *h) { return !h ? 0 : h->fused ? h->spl : 1; }
 
 const char *lbm_last_error(lbm_handle *h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 

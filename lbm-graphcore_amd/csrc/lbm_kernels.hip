@@ -362,17 +362,17 @@ __device__ __forceinline__ void ghost_cell(int e, int p, int w, int h, int &x, i
     }
 }
 
-// W2: strip cell (a, b) of direction d -> cell coordinates.
-__device__ __forceinline__ void strip_cell(int d, int a, int b, int w, int h, int &x, int &y) {
+// WG: strip cell (a, b) of direction d (width g) -> cell coordinates.
+__device__ __forceinline__ void strip_cell(int d, int a, int b, int w, int h, int g, int &x, int &y) {
     switch (d) {
-        case DE: x = w - 2 + a; y = b; break;
+        case DE: x = w - g + a; y = b; break;
         case DW: x = a; y = b; break;
-        case DN: x = b; y = h - 2 + a; break;
+        case DN: x = b; y = h - g + a; break;
         case DS: x = b; y = a; break;
-        case DNE: x = w - 2 + b; y = h - 2 + a; break;
-        case DNW: x = b; y = h - 2 + a; break;
+        case DNE: x = w - g + b; y = h - g + a; break;
+        case DNW: x = b; y = h - g + a; break;
         case DSW: x = b; y = a; break;
-        default: x = w - 2 + b; y = a; break;  // DSE
+        default: x = w - g + b; y = a; break;  // DSE
     }
 }
 
@@ -380,7 +380,7 @@ __device__ __forceinline__ int dev_edge_len(int d, int w, int h) { return d < 4 
 
 // Pack the outgoing halo of every direction in `mask` from the current
 // lattice to its destination (own ghost ring or send buffer).
-// Grid: (ceil(2*max(w,h)/BLOCK), 8).
+// Grid: (ceil(max(3, g)*max(w,h)/BLOCK), 8).
 __global__ __launch_bounds__(BLOCK) void halo_pack(HaloArgs a) {
     const int d = blockIdx.y;
     if (!((a.mask >> d) & 1u)) return;
@@ -398,11 +398,11 @@ __global__ __launch_bounds__(BLOCK) void halo_pack(HaloArgs a) {
             dst.p[s][(long long)pos * dst.ps] = src[k * a.plane];
         }
     } else {
-        const int len = d < 4 ? dev_edge_len(d, a.w, a.h) : 2;
-        if (i >= 2 * len) return;
+        const int len = d < 4 ? dev_edge_len(d, a.w, a.h) : a.g;
+        if (i >= a.g * len) return;
         const int sa = i / len, sb = i - sa * len;
         int x, y;
-        strip_cell(d, sa, sb, a.w, a.h, x, y);
+        strip_cell(d, sa, sb, a.w, a.h, a.g, x, y);
         const float *src = a.f + (long long)y * a.pitch + x;
         const Dst2 &dst = a.dst2[d];
         float *o = dst.base + (long long)sa * dst.s1 + (long long)sb * dst.s2;
@@ -430,15 +430,15 @@ __global__ __launch_bounds__(BLOCK) void halo_unpack(HaloArgs a) {
         }
     } else {
         // the neighbour on side e sent its strip of direction OPP(e), laid out
-        // [9][2][len] (edges) or [9][2][2] (corners)
-        const int len = e < 4 ? dev_edge_len(e, a.w, a.h) : 2;
-        if (i >= 2 * len) return;
+        // [9][g][len] (edges) or [9][g][g] (corners)
+        const int len = e < 4 ? dev_edge_len(e, a.w, a.h) : a.g;
+        if (i >= a.g * len) return;
         const int sa = i / len, sb = i - sa * len;
         const Dst2 &g = a.ghost2[e];
         float *o = g.base + (long long)sa * g.s1 + (long long)sb * g.s2;
         const float *r = a.recv[e] + (long long)sa * len + sb;
 #pragma unroll
-        for (int k = 0; k < Q; ++k) o[k * g.ks] = r[(long long)k * 2 * len];
+        for (int k = 0; k < Q; ++k) o[k * g.ks] = r[(long long)k * a.g * len];
     }
 }
 
@@ -494,13 +494,13 @@ hipError_t launch_soa_to_aos(const float *f, float *aos, long long P, int pitch,
 }
 
 hipError_t launch_halo_pack(const HaloArgs &a, hipStream_t s) {
-    const int m = 2 * (a.w > a.h ? a.w : a.h);
+    const int m = (a.g > 3 ? a.g : 3) * (a.w > a.h ? a.w : a.h);
     hipLaunchKernelGGL(halo_pack, dim3((m + BLOCK - 1) / BLOCK, 8), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_halo_unpack(const HaloArgs &a, hipStream_t s) {
-    const int m = 2 * (a.w > a.h ? a.w : a.h);
+    const int m = (a.g > 3 ? a.g : 3) * (a.w > a.h ? a.w : a.h);
     hipLaunchKernelGGL(halo_unpack, dim3((m + BLOCK - 1) / BLOCK, 8), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }

@@ -3,11 +3,12 @@
 // (lbm_engine.hip).
 //
 // Lattice (one per ping-pong side, per sub-domain of w x h cells): SoA with a
-// ghost ring GR = 2 cells wide.  Kernels address it through an ORIGIN pointer
+// ghost ring gr cells wide (engine: gr = max(2, halo width of the kernel in
+// use), at most MAX_GR).  Kernels address it through an ORIGIN pointer
 // o = &f[plane 0][cell (0,0)]:
 //     cell (x, y), -2 <= x < w+2, -2 <= y < h+2, speed k  ->  o[k*plane + y*pitch + x]
 // Default layout (row-interleaved): the nine planes of a lattice row are
-// adjacent, plane = rf, pitch = 9*rf, rf = roundup(w + XOFF + GR, 64); the
+// adjacent, plane = rf, pitch = 9*rf, rf = roundup(w + xoff + gr + 2, 64); the
 // planar layout (plane = rows*rf + pad, pitch = rf) is kept for A/B.  The
 // interior row start sits XOFF = 4 floats into each plane row, so every
 // interior float4 is 16-byte aligned.
@@ -21,10 +22,10 @@
 // Two halo formats:
 //   W1 (one-step kernels): the populations that leave through side d
 //       (PLANES[d]) of the outermost cell row/column, ghost ring width 1.
-//   W2 (two-step kernel): all nine populations of the two outermost cell
-//       rows/columns (2x2 cells at corners), ghost ring width 2 -- the
-//       intermediate step of a fused two-step launch recomputes one cell of
-//       halo, which pulls from two cells out.
+//   WG (multi-step kernels, width g = steps per launch): all nine
+//       populations of the g outermost cell rows/columns (g x g cells at
+//       corners) -- a fused S-step launch pulls from up to S cells out.
+//       (The fused two-step kernel is the g = 2 case, historically "W2".)
 #pragma once
 
 #include <cstdint>
@@ -33,7 +34,7 @@ namespace lbm {
 
 constexpr int Q = 9;
 constexpr int XOFF = 4;   // interior column 0 offset inside a plane row
-constexpr int GR = 2;     // ghost ring width (rows/columns)
+constexpr int MAX_GR = 4;  // widest ghost ring (rows/columns) any kernel needs
 constexpr int BLOCK = 256;  // 4 wave64s
 constexpr int MAX_RECTS = 4;
 
@@ -59,7 +60,7 @@ constexpr int PLANES[8][3] = {{1, 5, 8}, {2, 5, 6}, {3, 6, 7}, {4, 7, 8},
                               {5, -1, -1}, {6, -1, -1}, {7, -1, -1}, {8, -1, -1}};
 constexpr int NPLANES[8] = {3, 3, 3, 3, 1, 1, 1, 1};
 
-enum HaloMode : int { HALO_W1 = 1, HALO_W2 = 2 };
+enum HaloMode : int { HALO_W1 = 1, HALO_WG = 2 };
 
 // A rectangle of the sub-domain processed by one step launch, in work units
 // (one-step kernels: x0/y0 in cells, wc = width in lanes' chunks, hr = rows;
@@ -76,7 +77,7 @@ struct EdgeDst {
     int pad;
 };
 
-// W2 destination of one direction: value of speed k at strip coordinates
+// WG destination of one direction: value of speed k at strip coordinates
 // (a, b) -> base[k*ks + a*s1 + b*s2].  (a, b) = (strip column, row) for E/W,
 // (strip row, column) for N/S, (strip row, strip column) for corners.
 struct Dst2 {
@@ -135,6 +136,36 @@ struct Step2Args {
     int n_total, stride;
 };
 
+// S-step streaming kernels (lbm_stream.hip, lbm_stream2.hip): a rect of
+// output cells is cut into strips of ow columns (one wave each; ow = 64 - 2S
+// with one column per lane, 128 - 2S or 126 - 2S with two) and segments of
+// hs rows.
+struct SRect {
+    int x0, y0, w, h;   // output cells
+    int nstrip, hs;     // strips across, rows per segment
+    int ow;             // owned columns per strip
+};
+
+struct StreamArgs {
+    const float *fin;
+    float *fout;
+    const uint8_t *obst_g;  // ghosted obstacles, (y+og)*ogp + (x+og)
+    long long plane;
+    int pitch, ogp, og;
+    int w, h, xmax;         // xmax: last column inside the row allocation (>= w + gr + 1)
+    int gy0, ny, accel_g;
+    float omega, omo, w1, w2;
+    int nrect, total;       // total work units (strip x segment)
+    SRect rect[MAX_RECTS];
+    int rect_begin[MAX_RECTS];
+    Dst2 dst[8];            // WG halo destinations, g = S
+    float *partials_out;    // step s of this launch: partials_out[s*stride + blockIdx.x]
+    const float *partials_prev;
+    float *av_local;
+    int *ctl;
+    int n_total, stride;
+};
+
 // Halo pack (edge -> dst) after load / accelerate, and unpack (recv -> ghost
 // ring) after every exchange; both in either format.
 struct HaloArgs {
@@ -142,17 +173,18 @@ struct HaloArgs {
     long long plane;
     int pitch, w, h;
     unsigned mask;          // directions to process
-    int mode;               // HALO_W1 / HALO_W2
+    int mode;               // HALO_W1 / HALO_WG
+    int g;                  // WG width
     EdgeDst dst[8];         // W1 pack destinations
-    Dst2 dst2[8];           // W2 pack destinations
-    Dst2 ghost2[8];         // W2 unpack: ghost region of side e
+    Dst2 dst2[8];           // WG pack destinations
+    Dst2 ghost2[8];         // WG unpack: ghost region of side e
     const float *recv[8];   // unpack: receive buffer per direction
 };
 
 // message sizes (floats)
 inline int edge_len(int d, int w, int h) { return d < 4 ? ((d & 1) ? w : h) : 1; }
-inline long long msg_floats(int mode, int d, int w, int h) {
-    return mode == HALO_W2 ? (d < 4 ? 2LL * Q * edge_len(d, w, h) : 4LL * Q)
+inline long long msg_floats(int mode, int d, int w, int h, int g) {
+    return mode == HALO_WG ? (d < 4 ? (long long)g * Q * edge_len(d, w, h) : (long long)g * g * Q)
                            : (long long)NPLANES[d] * edge_len(d, w, h);
 }
 

@@ -31,12 +31,6 @@ __device__ __forceinline__ float accel_flag(const Step2Args &a, int y) {
     return (g == a.accel_g) ? 1.00f : 0.00f;
 }
 
-__device__ __forceinline__ void store2(const Dst2 &d, int sa, int sb, const float (&o)[Q]) {
-    float *p = d.base + (long long)sa * d.s1 + (long long)sb * d.s2;
-#pragma unroll
-    for (int k = 0; k < Q; ++k) p[k * d.ks] = o[k];
-}
-
 template <int T2W, int T2H, bool kReduce>
 __global__ __launch_bounds__(BLOCK) void step2(Step2Args a) {
     constexpr int MW = T2W + 2, MH = T2H + 2;

@@ -1,0 +1,298 @@
+// lbm_stream2.hip -- S-step register-streaming kernel, two columns per lane,
+// packed fp32 arithmetic.
+//
+// Same schedule as lbm_stream.hip (one wave walks a strip row by row, level L
+// computes row j-L of step t+L as input row j arrives; lattice through HBM
+// once per S steps), but each lane owns TWO adjacent columns (xa = base + 2l,
+// xb = xa + 1):
+//   * loads and stores are float2 (512 B per wave and plane row);
+//   * the x-1 / x+1 neighbours are half in-lane (B's left is A, A's right is
+//     B) and half one DPP wave shift away, so a shift costs one v_mov_dpp per
+//     two cells;
+//   * the two cells' arithmetic runs as packed fp32 (v_pk_add_f32 /
+//     v_pk_mul_f32 / v_pk_fma_f32 on ext_vector_type(2) float), halving the
+//     VALU instructions of the collision, which bounds the fused kernels;
+//   * a 128-column strip recomputes 2S (+2 when its first column has the
+//     wrong parity for float2 alignment) of every 128 columns instead of 2S
+//     of 64.
+//
+// Bitwise parity with the one-step kernels and the CPU oracle: every
+// expression is evaluated in the order of LastChance.cpp:226-262 with one
+// rounding per operation (packed ops round each lane like their scalar
+// forms; no contraction).  The three kinds of correctly rounded operations
+// use shorter exact sequences than the compiler's general expansions:
+//   * x / 9 and x / 36: q = x*y, r = fma(-d, q, x), q' = fma(r, y, q) with
+//     y = RN(1/d) -- exhaustively checked equal to RN(x/d) over 41 binades
+//     (every normal x with x/d normal behaves the same; tools/check_fastdiv.c);
+//   * n / rho: the LLVM AMDGPU IEEE division expansion (rcp, one Newton step,
+//     two residual corrections) minus its v_div_scale / v_div_fixup
+//     wrappers, which only act when an operand is within 2^64 of the
+//     exponent limits, 0, inf or NaN (densities are ~0.1 and momenta
+//     either 0 or far above 2^-100 in any physical state); the reciprocal
+//     refinement is shared by u_x and u_y;
+//   * sqrt(u^2): v_sqrt_f32 plus the LLVM one-ulp correction steps, without
+//     the 2^32 pre-scaling used only below 2^-96 (0 is still exact).
+// The GPU parity tests (bitwise lattice vs the oracle on every reference
+// grid and on randomized problems) check all of it end to end.
+
+#include "lbm_device.hpp"
+
+namespace lbm {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 mk2(float v) { return f2{v, v}; }
+
+__device__ __forceinline__ float dpp_from_left(float v) {  // lane - 1
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138 /* wave_shr:1 */, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {  // lane + 1
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130 /* wave_shl:1 */, 0xf, 0xf, false));
+}
+// (x-1) and (x+1) neighbours of a lane's column pair (A = .x, B = .y)
+__device__ __forceinline__ f2 left2(f2 v) { return f2{dpp_from_left(v.y), v.x}; }
+__device__ __forceinline__ f2 right2(f2 v) { return f2{v.y, dpp_from_right(v.x)}; }
+
+// RN(x / d) for d = 9 or 36 (see header)
+template <int D>
+__device__ __forceinline__ f2 div_const(f2 x) {
+    constexpr float y = 1.0f / (float)D;
+    const f2 q = x * mk2(y);
+    const f2 r = fma2(mk2(-(float)D), q, x);
+    return fma2(r, mk2(y), q);
+}
+
+// RN(nx / d), RN(ny / d) sharing the reciprocal refinement (see header)
+__device__ __forceinline__ void div_pair(f2 nx, f2 ny, f2 d, f2 &qx, f2 &qy) {
+    const f2 r0 = f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    const f2 nd = -d;
+    const f2 e = fma2(nd, r0, mk2(1.0f));
+    const f2 r = fma2(e, r0, r0);
+    f2 q = nx * r;
+    q = fma2(fma2(nd, q, nx), r, q);
+    qx = fma2(fma2(nd, q, nx), r, q);
+    f2 p = ny * r;
+    p = fma2(fma2(nd, p, ny), r, p);
+    qy = fma2(fma2(nd, p, ny), r, p);
+}
+
+// correctly rounded sqrt for 0 and normal x (see header)
+__device__ __forceinline__ float sqrt_cr(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __int_as_float(__float_as_int(s) - 1);
+    const float su = __int_as_float(__float_as_int(s) + 1);
+    const float rd = __builtin_fmaf(-sd, s, x);
+    const float ru = __builtin_fmaf(-su, s, x);
+    const float t = (rd <= 0.f) ? sd : s;
+    return (ru > 0.f) ? su : t;
+}
+
+// One cell pair: pulled populations s -> post-collision o; returns |u| per cell (0 for obstacles).
+__device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, float accf, float omega,
+                                       float omo, float w1, float w2) {
+    const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
+    f2 ux, uy;
+    div_pair(s[1] + s[5] + s[8] - (s[3] + s[6] + s[7]), s[2] + s[5] + s[6] - (s[4] + s[7] + s[8]), rho, ux, uy);
+    const f2 usq = ux * ux + uy * uy;
+    const f2 csq = mk2(1.00f) - usq * mk2(1.50f);
+    const f2 ld1 = div_const<9>(rho) * mk2(omega);
+    const f2 ld2 = div_const<36>(rho) * mk2(omega);
+    const f2 OMO = mk2(omo);
+    const f2 c23 = mk2(2.00f / 3.00f);
+    const f2 c45 = mk2(4.50f), n45 = mk2(-4.50f);
+
+    const f2 c0 = s[0] * OMO + mk2(4.00f / 9.00f) * rho * mk2(omega) * csq;
+    const f2 c1 = s[1] * OMO + ld1 * ((c45 * ux) * (c23 + ux) + csq);
+    const f2 c3 = s[3] * OMO + ld1 * ((n45 * ux) * (c23 - ux) + csq);
+    const f2 c2 = s[2] * OMO + ld1 * ((c45 * uy) * (c23 + uy) + csq);
+    const f2 c4 = s[4] * OMO + ld1 * ((n45 * uy) * (c23 - uy) + csq);
+    const f2 us = ux + uy;
+    const f2 c5 = s[5] * OMO + ld2 * ((c45 * us) * (c23 + us) + csq);
+    const f2 c7 = s[7] * OMO + ld2 * ((n45 * us) * (c23 - us) + csq);
+    const f2 ud = -ux + uy;
+    const f2 c6 = s[6] * OMO + ld2 * ((c45 * ud) * (c23 + ud) + csq);
+    const f2 c8 = s[8] * OMO + ld2 * ((n45 * ud) * (c23 - ud) + csq);
+    const f2 a1 = mk2(accf * w1), a2 = mk2(accf * w2);
+    const f2 f1 = c1 + a1, f3 = c3 - a1, f5 = c5 + a2, f6 = c6 - a2, f7 = c7 - a2, f8 = c8 + a2;
+    // obstacle cells rebound: out_k = s_opp(k)
+    o[0] = f2{oa ? s[0].x : c0.x, ob ? s[0].y : c0.y};
+    o[1] = f2{oa ? s[3].x : f1.x, ob ? s[3].y : f1.y};
+    o[3] = f2{oa ? s[1].x : f3.x, ob ? s[1].y : f3.y};
+    o[2] = f2{oa ? s[4].x : c2.x, ob ? s[4].y : c2.y};
+    o[4] = f2{oa ? s[2].x : c4.x, ob ? s[2].y : c4.y};
+    o[5] = f2{oa ? s[7].x : f5.x, ob ? s[7].y : f5.y};
+    o[7] = f2{oa ? s[5].x : f7.x, ob ? s[5].y : f7.y};
+    o[6] = f2{oa ? s[8].x : f6.x, ob ? s[8].y : f6.y};
+    o[8] = f2{oa ? s[6].x : f8.x, ob ? s[6].y : f8.y};
+    return f2{oa ? 0.f : sqrt_cr(usq.x), ob ? 0.f : sqrt_cr(usq.y)};
+}
+
+__device__ __forceinline__ float stream2_accel(const StreamArgs &a, int y) {
+    int g = a.gy0 + y;
+    g = g < 0 ? g + a.ny : (g >= a.ny ? g - a.ny : g);
+    return (g == a.accel_g) ? 1.00f : 0.00f;
+}
+
+__device__ __forceinline__ void halo_out(const StreamArgs &a, int S, int x, int y, const float (&o)[Q]) {
+    const bool east = x >= a.w - S, west = x < S, north = y >= a.h - S, south = y < S;
+    if (east) store2(a.dst[DE], x - (a.w - S), y, o);
+    if (west) store2(a.dst[DW], x, y, o);
+    if (north) {
+        store2(a.dst[DN], y - (a.h - S), x, o);
+        if (east) store2(a.dst[DNE], y - (a.h - S), x - (a.w - S), o);
+        if (west) store2(a.dst[DNW], y - (a.h - S), x, o);
+    }
+    if (south) {
+        store2(a.dst[DS], y, x, o);
+        if (west) store2(a.dst[DSW], y, x, o);
+        if (east) store2(a.dst[DSE], y, x - (a.w - S), o);
+    }
+}
+
+template <int S, bool kReduce>
+__global__ __launch_bounds__(64, 2) void stream_steps2c(StreamArgs a) {
+    __shared__ float lds[1];
+    if (kReduce && blockIdx.x == 0) reduce_pending_n<64>(a.ctl, a.partials_prev, a.av_local, lds);
+
+    const int lane = threadIdx.x;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    f2 tot[S];
+#pragma unroll
+    for (int l = 0; l < S; ++l) tot[l] = mk2(0.f);
+
+    if (t < a.total) {
+        const int r = rect_of(a.rect_begin, t);
+        const SRect R = a.rect[r];
+        const int lt = t - a.rect_begin[r];
+        const int seg = lt / R.nstrip, strip = lt - seg * R.nstrip;
+        const int xo0 = R.x0 + strip * R.ow;             // first owned column
+        const int xo1 = min(xo0 + R.ow, R.x0 + R.w);     // past the last owned column
+        const int base = (xo0 - S) & ~1;                 // even: float2-aligned
+        const int xa = base + 2 * lane, xb = xa + 1;
+        const bool owna = xa >= xo0 && xa < xo1, ownb = xb >= xo0 && xb < xo1;
+        const int yo0 = R.y0 + seg * R.hs;
+        const int yo1 = min(yo0 + R.hs, R.y0 + R.h);
+        const int xca = min(xa, (a.xmax - 1) & ~1);
+        const long long P = a.plane;
+        const int pitch = a.pitch;
+        const float *src = a.fin + xca;
+        const uint8_t *obp = a.obst_g + (xca + a.og);
+        const int jlast = yo1 + S - 1;
+
+        f2 c0[S], c1[S], c3[S], a2[S], a5[S], a6[S], b2[S], b5[S], b6[S];
+#pragma unroll
+        for (int b = 0; b < S; ++b)
+            c0[b] = c1[b] = c3[b] = a2[b] = a5[b] = a6[b] = b2[b] = b5[b] = b6[b] = mk2(0.f);
+        unsigned oba = 0, obb = 0;
+
+        int j = yo0 - S;
+        f2 v[Q];
+        unsigned voa, vob;
+        {
+            const float *c = src + (long long)j * pitch;
+#pragma unroll
+            for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const f2 *>(c + k * P);
+            const uint8_t *oc = obp + (long long)(j + a.og) * a.ogp;
+            voa = oc[0];
+            vob = oc[1];
+        }
+        for (; j <= jlast; ++j) {
+            const int jn = min(j + 1, jlast);
+            f2 nv[Q];
+            const float *cn = src + (long long)jn * pitch;
+#pragma unroll
+            for (int k = 0; k < Q; ++k) nv[k] = *reinterpret_cast<const f2 *>(cn + k * P);
+            const uint8_t *ocn = obp + (long long)(jn + a.og) * a.ogp;
+            const unsigned nvoa = ocn[0], nvob = ocn[1];
+
+            oba = (oba << 1) | (voa != 0 ? 1u : 0u);
+            obb = (obb << 1) | (vob != 0 ? 1u : 0u);
+            f2 cur[Q];
+#pragma unroll
+            for (int k = 0; k < Q; ++k) cur[k] = v[k];
+#pragma unroll
+            for (int L = 1; L <= S; ++L) {
+                const int b = L - 1;
+                const int y = j - L;
+                const f2 s[Q] = {c0[b], c1[b], b2[b], c3[b], cur[4], b5[b], b6[b], right2(cur[7]), left2(cur[8])};
+                b2[b] = a2[b];
+                b5[b] = a5[b];
+                b6[b] = a6[b];
+                a2[b] = cur[2];
+                a5[b] = left2(cur[5]);
+                a6[b] = right2(cur[6]);
+                c0[b] = cur[0];
+                c1[b] = left2(cur[1]);
+                c3[b] = right2(cur[3]);
+
+                f2 o[Q];
+                const f2 u = collide2(s, o, (oba >> L) & 1u, (obb >> L) & 1u, stream2_accel(a, y), a.omega, a.omo,
+                                      a.w1, a.w2);
+                const bool rowlive = y >= yo0 && y < yo1;
+                if (rowlive) tot[b] += f2{owna ? u.x : 0.f, ownb ? u.y : 0.f};
+                if (L == S) {
+                    if (rowlive && (owna || ownb)) {
+                        float *w0 = a.fout + (long long)y * pitch + xa;
+                        if (owna && ownb) {
+#pragma unroll
+                            for (int k = 0; k < Q; ++k) *reinterpret_cast<f2 *>(w0 + k * P) = o[k];
+                        } else if (owna) {
+#pragma unroll
+                            for (int k = 0; k < Q; ++k) w0[k * P] = o[k].x;
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < Q; ++k) w0[k * P + 1] = o[k].y;
+                        }
+                        if (xa < S || xb >= a.w - S || y < S || y >= a.h - S) {
+                            float oa_[Q], ob_[Q];
+#pragma unroll
+                            for (int k = 0; k < Q; ++k) {
+                                oa_[k] = o[k].x;
+                                ob_[k] = o[k].y;
+                            }
+                            if (owna) halo_out(a, S, xa, y, oa_);
+                            if (ownb) halo_out(a, S, xb, y, ob_);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < Q; ++k) cur[k] = o[k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < Q; ++k) v[k] = nv[k];
+            voa = nvoa;
+            vob = nvob;
+        }
+    }
+
+#pragma unroll
+    for (int l = 0; l < S; ++l) {
+        float sum = tot[l].x + tot[l].y;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
+        if (lane == 0) a.partials_out[(long long)l * a.stride + blockIdx.x] = sum;
+    }
+    if (kReduce && blockIdx.x == 0 && lane == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
+}
+
+template <int S>
+static void launch_s2c(const StreamArgs &a, int blocks, bool reduce, hipStream_t s) {
+    if (reduce)
+        hipLaunchKernelGGL((stream_steps2c<S, true>), dim3(blocks), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((stream_steps2c<S, false>), dim3(blocks), dim3(64), 0, s, a);
+}
+
+hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s) {
+    switch (steps) {
+        case 2: launch_s2c<2>(a, blocks, reduce, s); break;
+        case 3: launch_s2c<3>(a, blocks, reduce, s); break;
+        case 4: launch_s2c<4>(a, blocks, reduce, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace lbm

@@ -23,7 +23,7 @@ Q = 9
 LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
 TRANSPORT_LOCAL, TRANSPORT_RCCL = 0, 1
-KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4, KERNEL_STEP2 = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4, KERNEL_STEP2, KERNEL_STREAM = 0, 1, 2, 3, 4
 FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP = 1, 2
 
 # every symbol include/lbm_hip.h declares
@@ -31,7 +31,7 @@ EXPORTED = [
     "lbm_abi_version", "lbm_partition", "lbm_halo_plan", "lbm_device_count", "lbm_rccl_unique_id",
     "lbm_create", "lbm_create_ex", "lbm_load_cells", "lbm_init_equilibrium",
     "lbm_run", "lbm_run_steps", "lbm_store", "lbm_last_run_seconds",
-    "lbm_total_free_cells", "lbm_local_rects", "lbm_kernel_in_use",
+    "lbm_total_free_cells", "lbm_local_rects", "lbm_kernel_in_use", "lbm_steps_per_launch",
     "lbm_last_error", "lbm_destroy",
 ]
 
@@ -69,6 +69,7 @@ class Config(ctypes.Structure):
         ("kernel", ctypes.c_int32),
         ("graph_steps", ctypes.c_int32),
         ("flags", ctypes.c_int32),
+        ("steps_per_launch", ctypes.c_int32),
     ]
 
 
@@ -111,6 +112,7 @@ def load_library() -> ctypes.CDLL:
         "lbm_total_free_cells": ([H], i64),
         "lbm_local_rects": ([H, ctypes.POINTER(Rect), i32, i32p], ctypes.c_int),
         "lbm_kernel_in_use": ([H], i32),
+        "lbm_steps_per_launch": ([H], i32),
         "lbm_last_error": ([H], ctypes.c_char_p),
         "lbm_destroy": ([H], None),
     }
@@ -168,7 +170,7 @@ class Engine:
     def __init__(self, params, obstacles: np.ndarray, num_gpus: int = 1, *, parts: int | None = None,
                  grid=(0, 0), transport: int = TRANSPORT_LOCAL, rank: int = 0, world: int = 1,
                  devices=None, unique_id: bytes | None = None, kernel: int = KERNEL_AUTO,
-                 graph_steps: int = 0, flags: int = 0):
+                 graph_steps: int = 0, flags: int = 0, steps_per_launch: int = 0):
         self._L = load_library()
         self.params = Params(int(params.nx), int(params.ny), int(params.max_iters), int(params.reynolds_dim),
                              float(params.density), float(params.accel), float(params.omega))
@@ -191,6 +193,7 @@ class Engine:
         cfg.kernel = kernel
         cfg.graph_steps = graph_steps
         cfg.flags = flags
+        cfg.steps_per_launch = int(steps_per_launch)
         rc = self._L.lbm_create_ex(ctypes.byref(self.params), obst.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
                                    ctypes.byref(cfg), ctypes.byref(self._h))
         if rc != LBM_OK:
@@ -239,8 +242,11 @@ class Engine:
         return [(q.x0, q.y0, q.w, q.h) for q in rects[:n.value]]
 
     def kernel_in_use(self) -> str:
-        return {KERNEL_SCALAR: "scalar", KERNEL_VEC4: "vec4", KERNEL_STEP2: "step2"}[
+        return {KERNEL_SCALAR: "scalar", KERNEL_VEC4: "vec4", KERNEL_STEP2: "step2", KERNEL_STREAM: "stream"}[
             int(self._L.lbm_kernel_in_use(self._h))]
+
+    def steps_per_launch(self) -> int:
+        return int(self._L.lbm_steps_per_launch(self._h))
 
     def close(self) -> None:
         if self._h:

@@ -26,7 +26,8 @@ from lbm_amd import io as lio  # noqa: E402
 from lbm_amd import native  # noqa: E402
 from bench import synthetic_obstacles  # noqa: E402
 
-KNOBS = ["LBM_LAYOUT", "LBM_MAX_BLOCKS", "LBM_GRAPH_STEPS", "LBM_TWO_STEP", "LBM_FORCE_EXCHANGE", "LBM_TILE2"]
+KNOBS = ["LBM_LAYOUT", "LBM_MAX_BLOCKS", "LBM_GRAPH_STEPS", "LBM_TWO_STEP", "LBM_FORCE_EXCHANGE", "LBM_TILE2",
+         "LBM_KERNEL", "LBM_STREAM_S", "LBM_STREAM_HS", "LBM_XOFF"]
 
 
 def parse_variant(s: str):
