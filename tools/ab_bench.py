@@ -2,7 +2,9 @@
 """A/B the step kernel's tuning knobs in ONE process (interleaved rounds).
 
 Each variant is a set of LBM_* environment knobs read by lbm_create_ex
-(LBM_LAYOUT, LBM_MAX_BLOCKS, LBM_GRAPH_STEPS, LBM_TWO_STEP, LBM_FORCE_EXCHANGE).  For every round,
+(LBM_KERNEL, LBM_STREAM_S/_V/_HS, LBM_TILE2, LBM_LAYOUT, LBM_MAX_BLOCKS,
+LBM_GRAPH_STEPS, LBM_TWO_STEP, LBM_FORCE_EXCHANGE, LBM_XOFF); every LBM_*
+variable is cleared before each variant.  For every round,
 every variant creates an engine on the same synthetic problem, warms up and
 times `steps` steps with the library's device events.  Prints one JSON line
 per variant with the median / min ms per step and GB/s (72 B per update).
@@ -25,9 +27,6 @@ sys.path[:0] = [str(ROOT), str(ROOT / "lbm-graphcore_amd")]
 from lbm_amd import io as lio  # noqa: E402
 from lbm_amd import native  # noqa: E402
 from bench import synthetic_obstacles  # noqa: E402
-
-KNOBS = ["LBM_LAYOUT", "LBM_MAX_BLOCKS", "LBM_GRAPH_STEPS", "LBM_TWO_STEP", "LBM_FORCE_EXCHANGE", "LBM_TILE2",
-         "LBM_KERNEL", "LBM_STREAM_S", "LBM_STREAM_HS", "LBM_XOFF"]
 
 
 def parse_variant(s: str):
@@ -57,7 +56,7 @@ def main():
     ref = None
     for rnd in range(a.rounds):
         for name, env in variants:
-            for k in KNOBS:
+            for k in [k for k in os.environ if k.startswith("LBM_")]:
                 os.environ.pop(k, None)
             os.environ.update(env)
             with native.Engine(p, obst, devices=[0]) as e:
