@@ -177,7 +177,7 @@ struct lbm_handle {
     int stream_v = 2;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32)
     int og = 4;              // ghost width of the obstacle map
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
-    bool auto_stream = false; // AUTO picks the stream kernel when sizes allow
+    bool auto_stream = true;  // AUTO picks the stream kernel when sizes allow (LBM_KERNEL=step2 to A/B)
     bool forked = false;     // boundary stream running ahead of s_comp (multi-sub-domain launches)
     bool force_exchange = false;
     int graph_steps = 8;     // replay graphs of 2*graph_steps launches on the single-domain path
@@ -511,8 +511,9 @@ struct lbm_handle {
     }
 
     // Stream-kernel work split of a sub-domain (cells).  Segment height by
-    // size: about 16 waves per CU over the interior, at least 4*spl rows so
-    // the 2*spl re-streamed rows per segment stay a small overhead.
+    // size: about 8192 waves over the interior (32 per CU; measured best at
+    // 8192^2, profiles/r01/stream/ab_v2.log), at least 4*spl rows so the
+    // 2*spl re-streamed rows per segment stay a modest overhead.
     void stream_split(const Sub &s, std::vector<SRect> &inr, std::vector<SRect> &bnd) const {
         const int S = spl, b = S;
         // owned columns per strip: 64 - 2S (one column per lane); 128 - 2S
@@ -526,7 +527,7 @@ struct lbm_handle {
         int hs = stream_hs;
         if (hs <= 0) {
             const long long strips = (std::max(x1 - x0, 1) + ow_of(x0) - 1) / ow_of(x0);
-            const long long target = 4096;
+            const long long target = 8192;
             hs = (int)std::max<long long>(4LL * S, (std::max(y1 - y0, 1) * strips + target - 1) / target);
         }
         auto mk = [&](int rx, int ry, int rw, int rh, int rhs) {
