@@ -44,7 +44,7 @@ namespace lbm {
 hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hipStream_t s);
 hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t s);
 hipError_t launch_stream(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
-hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
+hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
@@ -176,8 +176,10 @@ struct lbm_handle {
     int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
     int stream_v = 2;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32)
     int og = 4;              // ghost width of the obstacle map
+    int stream_waves = 2;    // LBM_STREAM_W: register target of the two-column kernel (waves per SIMD)
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
-    bool auto_stream = true;  // AUTO picks the stream kernel when sizes allow (LBM_KERNEL=step2 to A/B)
+    long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
+                                             // at least this large (smaller ones lack waves for it: step2)
     bool forked = false;     // boundary stream running ahead of s_comp (multi-sub-domain launches)
     bool force_exchange = false;
     int graph_steps = 8;     // replay graphs of 2*graph_steps launches on the single-domain path
@@ -220,6 +222,8 @@ struct lbm_handle {
         stream_s = std::min(std::max(env_int("LBM_STREAM_S", stream_s), 2), 4);
         stream_hs = std::max(0, env_int("LBM_STREAM_HS", stream_hs));
         stream_v = env_int("LBM_STREAM_V", stream_v) == 1 ? 1 : 2;
+        stream_waves = env_int("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
+        stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         if (const char *k = getenv("LBM_KERNEL")) {
             const std::string v(k);
             env_kernel = v == "stream" ? LBM_KERNEL_STREAM : v == "step2" ? LBM_KERNEL_STEP2
@@ -626,15 +630,16 @@ struct lbm_handle {
         const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch : stream_s;
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > 4))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2..4");
-        bool can_stream = fused && S >= 2 && S <= 4;
+        bool can_stream = fused && S >= 2 && S <= 4, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;
             if (r.w < mw || r.h < mh) can_stream = false;
+            if ((long long)r.w * r.h < stream_min_cells) big = false;
         }
         if (kernel == LBM_KERNEL_STREAM && !can_stream)
             throw lbm_failure(LBM_E_INVALID, "stream kernel needs fused launches and sub-domains of at least "
                                              "steps_per_launch cells (twice that across a decomposed dimension)");
-        use_stream = kernel == LBM_KERNEL_STREAM || (kernel == LBM_KERNEL_AUTO && auto_stream && can_stream);
+        use_stream = kernel == LBM_KERNEL_STREAM || (kernel == LBM_KERNEL_AUTO && can_stream && big);
         spl = use_stream ? S : 2;
         hw = spl;
         gr = std::max(2, hw);
@@ -707,6 +712,10 @@ struct lbm_handle {
         set_device(subs[0]);
         HIP_CHECK(hipEventCreate(&t0));
         HIP_CHECK(hipEventCreate(&t1));
+        if (!multi() && graph_steps > 0) {  // capture both parities now, not inside a timed run
+            (void)graph_for(0);
+            (void)graph_for(1);
+        }
     }
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
@@ -883,7 +892,8 @@ struct lbm_handle {
             const int n = interior ? s.n3_int : s.n3_bnd;
             if (n <= 0) return hipSuccess;
             const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
-            return stream_v == 1 ? launch_stream(a, n, spl, interior, st) : launch_stream2c(a, n, spl, interior, st);
+            return stream_v == 1 ? launch_stream(a, n, spl, interior, st)
+                                 : launch_stream2c(a, n, spl, interior, stream_waves, st);
         }
         if (fused_launch) {
             const int n = interior ? s.n2_int : s.n2_bnd;

@@ -44,11 +44,12 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 mk2(float v) { return f2{v, v}; }
 
+// lanes shifted in from outside the wave read 0 (bound_ctrl); no old-value init move
 __device__ __forceinline__ float dpp_from_left(float v) {  // lane - 1
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138 /* wave_shr:1 */, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float dpp_from_right(float v) {  // lane + 1
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130 /* wave_shl:1 */, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
 }
 // (x-1) and (x+1) neighbours of a lane's column pair (A = .x, B = .y)
 __device__ __forceinline__ f2 left2(f2 v) { return f2{dpp_from_left(v.y), v.x}; }
@@ -89,8 +90,10 @@ __device__ __forceinline__ float sqrt_cr(float x) {
 }
 
 // One cell pair: pulled populations s -> post-collision o; returns |u| per cell (0 for obstacles).
-__device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, float accf, float omega,
-                                       float omo, float w1, float w2) {
+// any_obst (wave-uniform): some lane of the wave has an obstacle cell in this
+// row; without one the rebound selects are skipped (same values).
+__device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, float accf,
+                                       float omega, float omo, float w1, float w2) {
     const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
     f2 ux, uy;
     div_pair(s[1] + s[5] + s[8] - (s[3] + s[6] + s[7]), s[2] + s[5] + s[6] - (s[4] + s[7] + s[8]), rho, ux, uy);
@@ -115,6 +118,18 @@ __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bo
     const f2 c8 = s[8] * OMO + ld2 * ((n45 * ud) * (c23 - ud) + csq);
     const f2 a1 = mk2(accf * w1), a2 = mk2(accf * w2);
     const f2 f1 = c1 + a1, f3 = c3 - a1, f5 = c5 + a2, f6 = c6 - a2, f7 = c7 - a2, f8 = c8 + a2;
+    if (!any_obst) {
+        o[0] = c0;
+        o[1] = f1;
+        o[3] = f3;
+        o[2] = c2;
+        o[4] = c4;
+        o[5] = f5;
+        o[7] = f7;
+        o[6] = f6;
+        o[8] = f8;
+        return f2{sqrt_cr(usq.x), sqrt_cr(usq.y)};
+    }
     // obstacle cells rebound: out_k = s_opp(k)
     o[0] = f2{oa ? s[0].x : c0.x, ob ? s[0].y : c0.y};
     o[1] = f2{oa ? s[3].x : f1.x, ob ? s[3].y : f1.y};
@@ -150,8 +165,8 @@ __device__ __forceinline__ void halo_out(const StreamArgs &a, int S, int x, int 
     }
 }
 
-template <int S, bool kReduce>
-__global__ __launch_bounds__(64, 2) void stream_steps2c(StreamArgs a) {
+template <int S, bool kReduce, int MINW>
+__global__ __launch_bounds__(64, MINW) void stream_steps2c(StreamArgs a) {
     __shared__ float lds[1];
     if (kReduce && blockIdx.x == 0) reduce_pending_n<64>(a.ctl, a.partials_prev, a.av_local, lds);
 
@@ -227,8 +242,9 @@ __global__ __launch_bounds__(64, 2) void stream_steps2c(StreamArgs a) {
                 c3[b] = right2(cur[3]);
 
                 f2 o[Q];
-                const f2 u = collide2(s, o, (oba >> L) & 1u, (obb >> L) & 1u, stream2_accel(a, y), a.omega, a.omo,
-                                      a.w1, a.w2);
+                const bool oa = (oba >> L) & 1u, ob = (obb >> L) & 1u;
+                const bool any_obst = __builtin_amdgcn_ballot_w64(oa || ob) != 0;
+                const f2 u = collide2(s, o, oa, ob, any_obst, stream2_accel(a, y), a.omega, a.omo, a.w1, a.w2);
                 const bool rowlive = y >= yo0 && y < yo1;
                 if (rowlive) tot[b] += f2{owna ? u.x : 0.f, ownb ? u.y : 0.f};
                 if (L == S) {
@@ -277,19 +293,22 @@ __global__ __launch_bounds__(64, 2) void stream_steps2c(StreamArgs a) {
     if (kReduce && blockIdx.x == 0 && lane == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
 }
 
-template <int S>
+template <int S, int MINW>
 static void launch_s2c(const StreamArgs &a, int blocks, bool reduce, hipStream_t s) {
     if (reduce)
-        hipLaunchKernelGGL((stream_steps2c<S, true>), dim3(blocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2c<S, true, MINW>), dim3(blocks), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((stream_steps2c<S, false>), dim3(blocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2c<S, false, MINW>), dim3(blocks), dim3(64), 0, s, a);
 }
 
-hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s) {
+// waves = minimum waves per SIMD the register allocation targets (2, or 3:
+// fewer registers, some spilled)
+hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s) {
+    const bool w3 = waves >= 3;
     switch (steps) {
-        case 2: launch_s2c<2>(a, blocks, reduce, s); break;
-        case 3: launch_s2c<3>(a, blocks, reduce, s); break;
-        case 4: launch_s2c<4>(a, blocks, reduce, s); break;
+        case 2: launch_s2c<2, 2>(a, blocks, reduce, s); break;
+        case 3: w3 ? launch_s2c<3, 3>(a, blocks, reduce, s) : launch_s2c<3, 2>(a, blocks, reduce, s); break;
+        case 4: w3 ? launch_s2c<4, 3>(a, blocks, reduce, s) : launch_s2c<4, 2>(a, blocks, reduce, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
