@@ -2,7 +2,7 @@
 // top of the HIP engine's C ABI instead of a Poplar Engine.
 //
 //   lbm_runner --params P --obstacles O [-n N] [--device gpu|loopback] [-d] [--exe ignored]
-//              [--runs 5] [--kernel auto|scalar|vec4] [--out-dir DIR]
+//              [--runs 5] [--kernel auto|stream|step2|vec4|scalar] [--spl S] [--out-dir DIR]
 //
 // Flow (same program numbering as the reference):
 //   load params/obstacles -> initialise cells on host -> create engine
@@ -34,9 +34,10 @@ void usage(const char *exe) {
               << "      --params arg     filename of parameters file\n"
               << "      --obstacles arg  filename of obstacles file\n"
               << "      --runs arg       timed re-runs after the first (default: 5)\n"
-              << "      --kernel arg     auto, scalar or vec4 (default: auto)\n"
+              << "      --kernel arg     auto, stream, step2, vec4 or scalar (default: auto; vec4/scalar = one step per launch)\n"
+              << "      --spl arg        stream kernel: time steps per launch, 2..4 (default: library choice)\n"
               << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n"
-              << "      --graph-steps arg  replay the step loop as hipGraphs of 2*arg steps (default: 0 = off)\n"
+              << "      --graph-steps arg  replay the step loop as hipGraphs of 2*arg launches (0 = library default, <0 = off)\n"
               << "      --dump-partitioning arg  write the sub-domain decomposition as JSON\n";
 }
 
@@ -44,6 +45,7 @@ void usage(const char *exe) {
 
 int main(int argc, char *argv[]) {
     std::string paramsFile, obstaclesFile, device = "gpu", exeFile, kernel = "auto", outDir = ".", dumpFile;
+    int spl = 0;
     int numGpus = 1, runs = 5, graphSteps = 0;
     bool debug = false;
     for (int i = 1; i < argc; ++i) {
@@ -79,6 +81,14 @@ int main(int argc, char *argv[]) {
             runs = std::atoi(v.c_str());
         } else if (a == "--kernel") {
             if (!next(kernel)) { usage(argv[0]); return EXIT_FAILURE; }
+            if (kernel != "auto" && kernel != "stream" && kernel != "step2" && kernel != "vec4" && kernel != "scalar") {
+                usage(argv[0]);
+                return EXIT_FAILURE;
+            }
+        } else if (a == "--spl") {
+            std::string v;
+            if (!next(v)) { usage(argv[0]); return EXIT_FAILURE; }
+            spl = std::atoi(v.c_str());
         } else if (a == "--out-dir") {
             if (!next(outDir)) { usage(argv[0]); return EXIT_FAILURE; }
         } else if (a == "--graph-steps") {
@@ -161,7 +171,13 @@ int main(int argc, char *argv[]) {
         cfg.transport = LBM_TRANSPORT_LOCAL;
         cfg.devices = devs.empty() ? nullptr : devs.data();
         cfg.num_devices = (int32_t)devs.size();
-        cfg.kernel = kernel == "scalar" ? LBM_KERNEL_SCALAR : (kernel == "vec4" ? LBM_KERNEL_VEC4 : LBM_KERNEL_AUTO);
+        cfg.kernel = kernel == "scalar" ? LBM_KERNEL_SCALAR
+                   : kernel == "vec4"   ? LBM_KERNEL_VEC4
+                   : kernel == "step2"  ? LBM_KERNEL_STEP2
+                   : kernel == "stream" ? LBM_KERNEL_STREAM
+                                        : LBM_KERNEL_AUTO;
+        if (kernel == "scalar" || kernel == "vec4") cfg.flags |= LBM_FLAG_ONE_STEP;
+        cfg.steps_per_launch = spl;
         cfg.graph_steps = graphSteps;
         lbmhost::check(lbm_create_ex(&abi, obstacles->data.data(), &cfg, &h), nullptr, "lbm_create_ex");
     });
@@ -172,7 +188,10 @@ int main(int argc, char *argv[]) {
         for (int i = 0; i < n; ++i)
             std::cout << "sub-domain " << i << ": " << rects[i].w << "x" << rects[i].h << " at (row:" << rects[i].y0
                       << ",col:" << rects[i].x0 << ")" << std::endl;
-        std::cout << "step kernel: " << (lbm_kernel_in_use(h) == LBM_KERNEL_VEC4 ? "vec4" : "scalar") << std::endl;
+        const int32_t k = lbm_kernel_in_use(h);
+        std::cout << "step kernel: "
+                  << (k == LBM_KERNEL_STREAM ? "stream" : k == LBM_KERNEL_STEP2 ? "step2" : k == LBM_KERNEL_VEC4 ? "vec4" : "scalar")
+                  << " (" << lbm_steps_per_launch(h) << " steps per launch)" << std::endl;
     }
     lbmhost::timedStep("Running copy to device step", [&]() {
         lbmhost::check(lbm_load_cells(h, cells.data()), h, "lbm_load_cells");

@@ -135,6 +135,9 @@ def test_runner_cli_errors():
     assert r.returncode != 0 and "Could not parse parameters file" in r.stderr
     r = subprocess.run([str(PKG / "build" / "compare_lbm")], capture_output=True, text=True)
     assert r.returncode != 0 and "Usage" in r.stderr
+    r = subprocess.run([str(exe), "--params", "p", "--obstacles", "o", "--kernel", "bogus"], capture_output=True,
+                       text=True)
+    assert r.returncode != 0 and "--kernel" in r.stderr
 
 
 # ---------------------------------------------------------------- I/O ----

@@ -26,7 +26,9 @@ def _gate(tmp_path, grid):
 
 @pytest.mark.parametrize("args", [["-n", "1"], ["-n", "4", "--device", "loopback"],
                                   ["-n", "1", "--graph-steps", "50"], ["-n", "2", "--device", "loopback",
-                                                                      "--kernel", "scalar"]])
+                                                                      "--kernel", "scalar"],
+                                  ["-n", "1", "--kernel", "stream", "--spl", "3"],
+                                  ["-n", "4", "--device", "loopback", "--kernel", "stream"]])
 def test_lbm_runner_128(gpu_lib, tmp_path, args):
     exe = PKG / "build" / "lbm_runner"
     r = subprocess.run([str(exe), "--params", str(GOLD / "params" / "input_128x128.params"),
@@ -35,6 +37,8 @@ def test_lbm_runner_128(gpu_lib, tmp_path, args):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr
     assert "==done==" in r.stdout and "Reynolds number:" in r.stdout and "MLUPS:" in r.stdout
+    if "--kernel" in args:
+        assert f"step kernel: {args[args.index('--kernel') + 1]}" in r.stdout
     re_out = float(re.search(r"Reynolds number:\s+(\S+)", r.stdout).group(1))
     assert re_out == pytest.approx(oracle_manifest("128x128")["reynolds_last_av"], rel=2e-4)
     res = _gate(tmp_path, "128x128")
