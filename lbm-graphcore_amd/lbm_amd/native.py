@@ -19,6 +19,7 @@ PKG_ROOT = Path(__file__).resolve().parent.parent          # lbm-graphcore_amd/
 LIB_PATH = Path(os.environ.get("LBM_HIP_LIB", PKG_ROOT / "build" / "liblbm_hip.so"))
 
 Q = 9
+ABI_VERSION = 2          # LBM_ABI_VERSION in include/lbm_hip.h
 
 LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
@@ -120,6 +121,8 @@ def load_library() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    if L.lbm_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI version {L.lbm_abi_version()}, binding expects {ABI_VERSION}")
     _lib = L
     return L
 
