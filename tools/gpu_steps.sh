@@ -1,20 +1,24 @@
 #!/bin/bash
-# Run GPU steps in order, each under its own time limit; stop at the first
-# step that crashes, aborts or times out (exit >= 124 or a signal), so nothing
-# more touches the GPU after a fault.  A plain test failure (exit 1) does not
-# stop later steps.  Usage: tools/gpu_steps.sh "secs|name|command" ...
+# Run GPU steps one after another on the gpurun box, each under its own time
+# limit, logging to gpurun_out/<name>.log.  Stops at the first failing step
+# (fault, abort, timeout) so nothing more touches the GPU after trouble.
+#
+#   bash tools/gpu_steps.sh "SECONDS|name|command" ["SECONDS|name|command" ...]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
 mkdir -p gpurun_out
 for spec in "$@"; do
-  secs="${spec%%|*}"; rest="${spec#*|}"; name="${rest%%|*}"; cmd="${rest#*|}"
-  echo "=== [$name] (limit ${secs}s): $cmd" | tee -a gpurun_out/steps.log
+  secs="${spec%%|*}"; rest="${spec#*|}"
+  name="${rest%%|*}"; cmd="${rest#*|}"
+  echo "=== [$name] ($secs s) $cmd"
   start=$(date +%s)
   timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
   rc=$?
-  echo "=== [$name] rc=$rc in $(( $(date +%s) - start ))s" | tee -a gpurun_out/steps.log
-  tail -n 15 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then
-    echo "=== stopping after [$name] (rc=$rc)" | tee -a gpurun_out/steps.log
+  echo "=== [$name] rc=$rc in $(( $(date +%s) - start )) s"
+  tail -n 4 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then
+    echo "=== stopping after failed step $name"
     exit $rc
   fi
 done
-exit 0
+echo "=== all steps ok"
