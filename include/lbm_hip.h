@@ -57,10 +57,20 @@ enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
 /* Step kernels.  SCALAR / VEC4: one time step per launch (VEC4 needs widths
  * that are multiples of 4).  STEP2: fused two-step launches through LDS.
  * STREAM: fused S-step launches (S = steps_per_launch, 2..4) streaming rows
- * through registers.  AUTO picks the fastest kernel the sub-domain sizes
- * allow; lbm_kernel_in_use reports the choice.  LBM_FLAG_ONE_STEP forces one
- * step per launch. */
-enum { LBM_KERNEL_AUTO = 0, LBM_KERNEL_SCALAR = 1, LBM_KERNEL_VEC4 = 2, LBM_KERNEL_STEP2 = 3, LBM_KERNEL_STREAM = 4 };
+ * through registers.  RESIDENT: every step of a run in one persistent
+ * launch with the lattice held on chip (LDS + registers) -- single
+ * sub-domain grids small enough for all of their 64-column tiles to be
+ * co-resident (1024x1024 and below on MI355X).  AUTO picks the fastest
+ * kernel the sub-domain sizes allow; lbm_kernel_in_use reports the choice.
+ * LBM_FLAG_ONE_STEP forces one step per launch. */
+enum {
+    LBM_KERNEL_AUTO = 0,
+    LBM_KERNEL_SCALAR = 1,
+    LBM_KERNEL_VEC4 = 2,
+    LBM_KERNEL_STEP2 = 3,
+    LBM_KERNEL_STREAM = 4,
+    LBM_KERNEL_RESIDENT = 5
+};
 
 /*
  * Placement of the 2-D block decomposition.
@@ -192,8 +202,10 @@ int64_t lbm_total_free_cells(lbm_handle *h);
 /* Local sub-domain rectangles of this handle (LOCAL: all; RCCL: this rank's). */
 int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *n_out);
 
-/* Which step kernel the handle uses (LBM_KERNEL_STREAM, _STEP2, _VEC4 or
- * _SCALAR), and how many time steps one of its launches advances. */
+/* Which step kernel the handle uses (LBM_KERNEL_RESIDENT, _STREAM, _STEP2,
+ * _VEC4 or _SCALAR), and how many time steps one of its launches advances
+ * (RESIDENT: all steps of a run -- the last run's count, max_iters before
+ * the first run). */
 int32_t lbm_kernel_in_use(lbm_handle *h);
 int32_t lbm_steps_per_launch(lbm_handle *h);
 

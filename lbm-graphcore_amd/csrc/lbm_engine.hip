@@ -54,6 +54,9 @@ hipError_t launch_aos_to_soa(const float *aos, float *f, long long P, int pitch,
 hipError_t launch_soa_to_aos(const float *f, float *aos, long long P, int pitch, int w, int h, hipStream_t s);
 hipError_t launch_halo_pack(const HaloArgs &a, hipStream_t s);
 hipError_t launch_halo_unpack(const HaloArgs &a, hipStream_t s);
+hipError_t resident_capacity(int variant, int device, int &capacity);
+hipError_t launch_resident(const ResidentArgs &a, int variant, hipStream_t s);
+hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s);
 }  // namespace lbm
 
 using namespace lbm;
@@ -180,6 +183,19 @@ struct lbm_handle {
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
+    // lattice-resident persistent kernel (lbm_resident.hip): single sub-domain only
+    bool resident = false;
+    int res_variant = -1;    // ResVariant (LBM_RES_TH picks the tile height)
+    int res_th_env = 0;
+    int res_version = 0;     // LBM_RES_V: 1 = scalar 64-column tiles, 2 = packed 128-column tiles, 0 = by grid
+    int res_tx = 0, res_ty = 0;
+    unsigned long long *res_halo = nullptr;
+    float *res_partials = nullptr;
+    long long res_partials_cap = 0;
+    int *res_status = nullptr;
+    unsigned res_tag = 0;    // granule tags used so far (each run continues the sequence)
+    long long res_timeout = 0;
+    long long resident_max_cells = 1LL << 20;  // LBM_RES_MAX_CELLS: AUTO uses the resident kernel up to this size
     bool forked = false;     // boundary stream running ahead of s_comp (multi-sub-domain launches)
     bool force_exchange = false;
     int graph_steps = 8;     // replay graphs of 2*graph_steps launches on the single-domain path
@@ -224,9 +240,13 @@ struct lbm_handle {
         stream_v = env_int("LBM_STREAM_V", stream_v) == 1 ? 1 : 2;
         stream_waves = env_int("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
         stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
+        res_th_env = std::max(0, env_int("LBM_RES_TH", 0));
+        res_version = env_int("LBM_RES_V", 0);
+        resident_max_cells = std::max(0, env_int("LBM_RES_MAX_CELLS", (int)resident_max_cells));
         if (const char *k = getenv("LBM_KERNEL")) {
             const std::string v(k);
-            env_kernel = v == "stream" ? LBM_KERNEL_STREAM : v == "step2" ? LBM_KERNEL_STEP2
+            env_kernel = v == "resident" ? LBM_KERNEL_RESIDENT
+                       : v == "stream" ? LBM_KERNEL_STREAM : v == "step2" ? LBM_KERNEL_STEP2
                        : v == "vec4" ? LBM_KERNEL_VEC4 : v == "scalar" ? LBM_KERNEL_SCALAR : -1;
         }
         const char *l = getenv("LBM_LAYOUT");
@@ -708,14 +728,153 @@ struct lbm_handle {
             set_device(s);
             build_args(s);
         }
+        // lattice-resident kernel: one sub-domain whose 64-column tiles can all be co-resident
+        const bool res_ok = parts == 1 && !force_exchange && subs.size() == 1;
+        if (kernel == LBM_KERNEL_RESIDENT && !res_ok)
+            throw lbm_failure(LBM_E_INVALID, "resident kernel needs a single sub-domain without forced exchange");
+        if (res_ok && (kernel == LBM_KERNEL_RESIDENT ||
+                       (kernel == LBM_KERNEL_AUTO && (long long)p.nx * p.ny <= resident_max_cells))) {
+            resident = setup_resident(subs[0]);
+            if (kernel == LBM_KERNEL_RESIDENT && !resident)
+                throw lbm_failure(LBM_E_INVALID, "resident kernel: the grid's tiles cannot all be co-resident on the device");
+        }
         ensure_av(std::max(p.max_iters, 1));
         set_device(subs[0]);
         HIP_CHECK(hipEventCreate(&t0));
         HIP_CHECK(hipEventCreate(&t1));
-        if (!multi() && graph_steps > 0) {  // capture both parities now, not inside a timed run
+        if (!resident && !multi() && graph_steps > 0) {  // capture both parities now, not inside a timed run
             (void)graph_for(0);
             (void)graph_for(1);
         }
+    }
+
+    // Pick the resident tile height (smallest with at most one tile per CU,
+    // or LBM_RES_TH) and allocate the granule buffer.  false: does not fit.
+    bool setup_resident(const Sub &s) {
+        set_device(s);
+        int cus = 0;
+        HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev));
+        // v2 (packed pairs, 128-column tiles) needs an even width; v1 takes any grid
+        std::vector<int> order;
+        // (smallest tile height with one tile per CU first, except that 2-row
+        // tiles are slower than 4-row ones on every grid measured:
+        // profiles/r01/resident/)
+        if (p.nx % 2 == 0 && res_version != 1) order = {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2};
+        if (res_version != 2) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});
+        res_variant = -1;
+        for (int v : order) {
+            if (res_th_env > 0 && RES_TH[v] != res_th_env) continue;
+            const int tx = (p.nx + RES_TWV[v] - 1) / RES_TWV[v];
+            const int ty = (p.ny + RES_TH[v] - 1) / RES_TH[v];
+            int cap = 0;
+            HIP_CHECK(resident_capacity(v, s.dev, cap));
+            const long long n = (long long)tx * ty;
+            if (n <= cap && n <= cus) {
+                res_variant = v;
+                res_tx = tx;
+                res_ty = ty;
+                break;
+            }
+        }
+        if (res_variant < 0) return false;
+        const size_t granules = 2ull * res_tx * res_ty * 8 * 3 * RES_GW;
+        HIP_CHECK(hipMalloc(&res_halo, granules * sizeof(unsigned long long)));
+        HIP_CHECK(hipMemset(res_halo, 0, granules * sizeof(unsigned long long)));
+        HIP_CHECK(hipMalloc(&res_status, 64));
+        HIP_CHECK(hipMemset(res_status, 0, 64));
+        int khz = 0;
+        HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.dev));
+        res_timeout = (long long)std::max(khz, 1000) * 2000;  // 2 s of wall clock per poll phase
+        return true;
+    }
+
+    // Every step of the run in one cooperative launch (lbm_resident.hip),
+    // then the fixed-order |u| fold.  The ghost ring of the result is not
+    // maintained (only the resident kernel runs on this handle).
+    void run_resident(int steps, bool accelerate_first) {
+        Sub &s = subs[0];
+        set_device(s);
+        const int ntiles = res_tx * res_ty;
+        if ((long long)steps * ntiles > res_partials_cap) {
+            if (res_partials) HIP_CHECK(hipFree(res_partials));
+            res_partials = nullptr;
+            res_partials_cap = (long long)std::max(steps, 1) * ntiles;
+            HIP_CHECK(hipMalloc(&res_partials, sizeof(float) * (size_t)res_partials_cap));
+        }
+        HIP_CHECK(hipMemsetAsync(res_status, 0, 64, s.s_comp));
+        HIP_CHECK(hipEventRecord(t0, s.s_comp));
+        if (accelerate_first && s.accel_row >= 0) {
+            const float w1 = p.density * p.accel / 9.f;
+            const float w2 = p.density * p.accel / 36.f;
+            HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+        }
+        if (steps > 0) {
+            ResidentArgs a{};
+            a.fin = s.o[s.cur];
+            a.fout = s.o[1 - s.cur];
+            a.obst = s.obst;
+            a.plane = s.plane;
+            a.pitch = s.pitch;
+            a.nx = p.nx;
+            a.ny = p.ny;
+            a.tiles_x = res_tx;
+            a.tiles_y = res_ty;
+            a.steps = steps;
+            a.tag0 = res_tag;
+            a.accel_row = p.ny >= 2 ? p.ny - 2 : -1;
+            a.omega = p.omega;
+            a.omo = 1 - p.omega;
+            a.w1 = p.density * p.accel / 9.f;
+            a.w2 = p.density * p.accel / 36.f;
+            a.halo = res_halo;
+            a.partials = res_partials;
+            a.status = res_status;
+            a.timeout_ticks = res_timeout;
+            long long *trace = nullptr;
+            const int trace_steps = std::min(steps, 256);
+            if (env_int("LBM_RES_TRACE", 0)) {
+                HIP_CHECK(hipMalloc(&trace, sizeof(long long) * 5 * trace_steps));
+                HIP_CHECK(hipMemsetAsync(trace, 0, sizeof(long long) * 5 * trace_steps, s.s_comp));
+                a.trace = trace;
+                a.trace_steps = trace_steps;
+            }
+            HIP_CHECK(launch_resident(a, res_variant, s.s_comp));
+            if (trace) {  // mean phase durations over the traced steps (skipping the first)
+                std::vector<long long> tv((size_t)5 * trace_steps);
+                HIP_CHECK(hipMemcpyAsync(tv.data(), trace, tv.size() * sizeof(long long), hipMemcpyDeviceToHost, s.s_comp));
+                HIP_CHECK(hipStreamSynchronize(s.s_comp));
+                HIP_CHECK(hipFree(trace));
+                double ph[5] = {0, 0, 0, 0, 0};
+                int n = 0;
+                for (int t = 1; t + 1 < trace_steps; ++t, ++n) {
+                    const long long *r = &tv[(size_t)5 * t];
+                    ph[0] += (double)(r[1] - r[0]);
+                    ph[1] += (double)(r[2] - r[1]);
+                    ph[2] += (double)(r[3] - r[2]);
+                    ph[3] += (double)(r[4] - r[3]);
+                    ph[4] += (double)(tv[(size_t)5 * (t + 1)] - r[0]);
+                }
+                int khz = 1;
+                HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.dev));
+                const double us = 1e3 / khz / std::max(n, 1);
+                fprintf(stderr, "[resident trace] %dx%d tile-height %d: per step (us) pull+barrier %.3f collide+publish %.3f "
+                        "poll %.3f barrier %.3f total %.3f\n", p.nx, p.ny, RES_TH[res_variant], ph[0] * us, ph[1] * us,
+                        ph[2] * us, ph[3] * us, ph[4] * us);
+            }
+            res_tag += (unsigned)steps;
+            HIP_CHECK(launch_resident_reduce(res_partials, s.av_local, steps, ntiles, s.s_comp));
+            s.cur ^= 1;
+        }
+        HIP_CHECK(hipEventRecord(t1, s.s_comp));
+        HIP_CHECK(hipEventSynchronize(t1));
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, t0, t1));
+        int status = 0;
+        HIP_CHECK(hipMemcpy(&status, res_status, sizeof(int), hipMemcpyDeviceToHost));
+        if (status != 0)
+            throw lbm_failure(LBM_E_INTERNAL, "resident kernel: a neighbour hand-off timed out (tiles not co-resident?)");
+        last_seconds = ms * 1e-3;
+        last_steps = steps;
     }
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
@@ -1004,6 +1163,10 @@ struct lbm_handle {
         if (!loaded) throw lbm_failure(LBM_E_STATE, "lattice not initialised (call lbm_load_cells or lbm_init_equilibrium)");
         if (steps < 0) throw lbm_failure(LBM_E_INVALID, "steps must be >= 0");
         ensure_av(std::max(steps, 1));
+        if (resident) {
+            run_resident(steps, accelerate_first);
+            return;
+        }
         for (auto &s : subs) {
             set_device(s);
             HIP_CHECK(hipMemsetAsync(s.ctl, 0, 64, s.s_comp));
@@ -1173,6 +1336,9 @@ struct lbm_handle {
             if (s.ev_u) (void)hipEventDestroy(s.ev_u);
             if (s.ev_end) (void)hipEventDestroy(s.ev_end);
         }
+        if (res_halo) (void)hipFree(res_halo);
+        if (res_partials) (void)hipFree(res_partials);
+        if (res_status) (void)hipFree(res_status);
         if (comm) (void)ncclCommDestroy(comm);
         if (t0) (void)hipEventDestroy(t0);
         if (t1) (void)hipEventDestroy(t1);
@@ -1319,11 +1485,16 @@ int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *
 
 int32_t lbm_kernel_in_use(lbm_handle *h) {
     if (!h) return LBM_KERNEL_SCALAR;
+    if (h->resident) return LBM_KERNEL_RESIDENT;
     if (h->fused) return h->use_stream ? LBM_KERNEL_STREAM : LBM_KERNEL_STEP2;
     return h->vec4 ? LBM_KERNEL_VEC4 : LBM_KERNEL_SCALAR;
 }
 
-int32_t lbm_steps_per_launch(lbm_handle *h) { return !h ? 0 : h->fused ? h->spl : 1; }
+int32_t lbm_steps_per_launch(lbm_handle *h) {
+    if (!h) return 0;
+    if (h->resident) return std::max(1, h->last_steps > 0 ? h->last_steps : h->p.max_iters);
+    return h->fused ? h->spl : 1;
+}
 
 const char *lbm_last_error(lbm_handle *h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 

@@ -166,6 +166,42 @@ struct StreamArgs {
     int n_total, stride;
 };
 
+// Lattice-resident persistent kernel (lbm_resident.hip): tiles of RES_TW
+// columns x RES_TH[variant] rows, one workgroup each, all co-resident; every
+// step of a run in one launch.  Edge populations move between neighbouring
+// tiles as 8-byte {value, tag} granules: halo[2][ntiles][8 dirs][3][RES_GW].
+// v1 (scalar, one column per lane): 64-column tiles, any grid.  v2 (packed
+// fp32, a column pair per lane): 128-column tiles, even nx only.
+constexpr int RES_TW = 64;
+constexpr int RES2_TW = 128;
+enum ResVariant : int {
+    RES_64 = 0, RES_32 = 1, RES_16 = 2, RES_16x4 = 3, RES_8 = 4, RES_4 = 5,           // v1
+    RES2_32 = 6, RES2_16 = 7, RES2_8 = 8, RES2_4 = 9, RES2_2 = 10                     // v2
+};
+constexpr int NUM_RES = 11;
+constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2};
+constexpr int RES_TWV[NUM_RES] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128};
+constexpr int RES_GW = 128;  // granule positions per (tile, direction, plane), both versions
+
+struct ResidentArgs {
+    const float *fin;       // input lattice origin (interior read, ring from periodic images)
+    float *fout;            // output lattice origin (interior written at the end)
+    const uint8_t *obst;    // uint8[ny][nx]
+    long long plane;
+    int pitch;
+    int nx, ny, tiles_x, tiles_y;
+    int steps;
+    unsigned tag0;          // granule tags of this run: tag0 + 1 .. tag0 + steps
+    int accel_row;          // global row with the folded acceleration (-1: none)
+    float omega, omo, w1, w2;
+    unsigned long long *halo;
+    float *partials;        // [steps][ntiles]
+    int *status;            // set to 1 when a neighbour hand-off timed out
+    long long timeout_ticks;  // wall-clock ticks a poll may wait
+    long long *trace;       // LBM_RES_TRACE diagnostics: [step][5] wall-clock stamps of tile 0, wave 0 (or null)
+    int trace_steps;
+};
+
 // Halo pack (edge -> dst) after load / accelerate, and unpack (recv -> ghost
 // ring) after every exchange; both in either format.
 struct HaloArgs {

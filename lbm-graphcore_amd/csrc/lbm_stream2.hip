@@ -16,132 +16,15 @@
 //     wrong parity for float2 alignment) of every 128 columns instead of 2S
 //     of 64.
 //
-// Bitwise parity with the one-step kernels and the CPU oracle: every
-// expression is evaluated in the order of LastChance.cpp:226-262 with one
-// rounding per operation (packed ops round each lane like their scalar
-// forms; no contraction).  The three kinds of correctly rounded operations
-// use shorter exact sequences than the compiler's general expansions:
-//   * x / 9 and x / 36: q = x*y, r = fma(-d, q, x), q' = fma(r, y, q) with
-//     y = RN(1/d) -- exhaustively checked equal to RN(x/d) over 41 binades
-//     (every normal x with x/d normal behaves the same; tools/check_fastdiv.c);
-//   * n / rho: the LLVM AMDGPU IEEE division expansion (rcp, one Newton step,
-//     two residual corrections) minus its v_div_scale / v_div_fixup
-//     wrappers, which only act when an operand is within 2^64 of the
-//     exponent limits, 0, inf or NaN (densities are ~0.1 and momenta
-//     either 0 or far above 2^-100 in any physical state); the reciprocal
-//     refinement is shared by u_x and u_y;
-//   * sqrt(u^2): v_sqrt_f32 plus the LLVM one-ulp correction steps, without
-//     the 2^32 pre-scaling used only below 2^-96 (0 is still exact).
+// Bitwise parity with the one-step kernels and the CPU oracle: the packed
+// collision and its exact short division / sqrt sequences live in
+// lbm_packed.hpp (shared with the packed resident kernel).
 // The GPU parity tests (bitwise lattice vs the oracle on every reference
 // grid and on randomized problems) check all of it end to end.
 
-#include "lbm_device.hpp"
+#include "lbm_packed.hpp"
 
 namespace lbm {
-
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 mk2(float v) { return f2{v, v}; }
-
-// lanes shifted in from outside the wave read 0 (bound_ctrl); no old-value init move
-__device__ __forceinline__ float dpp_from_left(float v) {  // lane - 1
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
-}
-__device__ __forceinline__ float dpp_from_right(float v) {  // lane + 1
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
-}
-// (x-1) and (x+1) neighbours of a lane's column pair (A = .x, B = .y)
-__device__ __forceinline__ f2 left2(f2 v) { return f2{dpp_from_left(v.y), v.x}; }
-__device__ __forceinline__ f2 right2(f2 v) { return f2{v.y, dpp_from_right(v.x)}; }
-
-// RN(x / d) for d = 9 or 36 (see header)
-template <int D>
-__device__ __forceinline__ f2 div_const(f2 x) {
-    constexpr float y = 1.0f / (float)D;
-    const f2 q = x * mk2(y);
-    const f2 r = fma2(mk2(-(float)D), q, x);
-    return fma2(r, mk2(y), q);
-}
-
-// RN(nx / d), RN(ny / d) sharing the reciprocal refinement (see header)
-__device__ __forceinline__ void div_pair(f2 nx, f2 ny, f2 d, f2 &qx, f2 &qy) {
-    const f2 r0 = f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    const f2 nd = -d;
-    const f2 e = fma2(nd, r0, mk2(1.0f));
-    const f2 r = fma2(e, r0, r0);
-    f2 q = nx * r;
-    q = fma2(fma2(nd, q, nx), r, q);
-    qx = fma2(fma2(nd, q, nx), r, q);
-    f2 p = ny * r;
-    p = fma2(fma2(nd, p, ny), r, p);
-    qy = fma2(fma2(nd, p, ny), r, p);
-}
-
-// correctly rounded sqrt for 0 and normal x (see header)
-__device__ __forceinline__ float sqrt_cr(float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sd = __int_as_float(__float_as_int(s) - 1);
-    const float su = __int_as_float(__float_as_int(s) + 1);
-    const float rd = __builtin_fmaf(-sd, s, x);
-    const float ru = __builtin_fmaf(-su, s, x);
-    const float t = (rd <= 0.f) ? sd : s;
-    return (ru > 0.f) ? su : t;
-}
-
-// One cell pair: pulled populations s -> post-collision o; returns |u| per cell (0 for obstacles).
-// any_obst (wave-uniform): some lane of the wave has an obstacle cell in this
-// row; without one the rebound selects are skipped (same values).
-__device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, float accf,
-                                       float omega, float omo, float w1, float w2) {
-    const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
-    f2 ux, uy;
-    div_pair(s[1] + s[5] + s[8] - (s[3] + s[6] + s[7]), s[2] + s[5] + s[6] - (s[4] + s[7] + s[8]), rho, ux, uy);
-    const f2 usq = ux * ux + uy * uy;
-    const f2 csq = mk2(1.00f) - usq * mk2(1.50f);
-    const f2 ld1 = div_const<9>(rho) * mk2(omega);
-    const f2 ld2 = div_const<36>(rho) * mk2(omega);
-    const f2 OMO = mk2(omo);
-    const f2 c23 = mk2(2.00f / 3.00f);
-    const f2 c45 = mk2(4.50f), n45 = mk2(-4.50f);
-
-    const f2 c0 = s[0] * OMO + mk2(4.00f / 9.00f) * rho * mk2(omega) * csq;
-    const f2 c1 = s[1] * OMO + ld1 * ((c45 * ux) * (c23 + ux) + csq);
-    const f2 c3 = s[3] * OMO + ld1 * ((n45 * ux) * (c23 - ux) + csq);
-    const f2 c2 = s[2] * OMO + ld1 * ((c45 * uy) * (c23 + uy) + csq);
-    const f2 c4 = s[4] * OMO + ld1 * ((n45 * uy) * (c23 - uy) + csq);
-    const f2 us = ux + uy;
-    const f2 c5 = s[5] * OMO + ld2 * ((c45 * us) * (c23 + us) + csq);
-    const f2 c7 = s[7] * OMO + ld2 * ((n45 * us) * (c23 - us) + csq);
-    const f2 ud = -ux + uy;
-    const f2 c6 = s[6] * OMO + ld2 * ((c45 * ud) * (c23 + ud) + csq);
-    const f2 c8 = s[8] * OMO + ld2 * ((n45 * ud) * (c23 - ud) + csq);
-    const f2 a1 = mk2(accf * w1), a2 = mk2(accf * w2);
-    const f2 f1 = c1 + a1, f3 = c3 - a1, f5 = c5 + a2, f6 = c6 - a2, f7 = c7 - a2, f8 = c8 + a2;
-    if (!any_obst) {
-        o[0] = c0;
-        o[1] = f1;
-        o[3] = f3;
-        o[2] = c2;
-        o[4] = c4;
-        o[5] = f5;
-        o[7] = f7;
-        o[6] = f6;
-        o[8] = f8;
-        return f2{sqrt_cr(usq.x), sqrt_cr(usq.y)};
-    }
-    // obstacle cells rebound: out_k = s_opp(k)
-    o[0] = f2{oa ? s[0].x : c0.x, ob ? s[0].y : c0.y};
-    o[1] = f2{oa ? s[3].x : f1.x, ob ? s[3].y : f1.y};
-    o[3] = f2{oa ? s[1].x : f3.x, ob ? s[1].y : f3.y};
-    o[2] = f2{oa ? s[4].x : c2.x, ob ? s[4].y : c2.y};
-    o[4] = f2{oa ? s[2].x : c4.x, ob ? s[2].y : c4.y};
-    o[5] = f2{oa ? s[7].x : f5.x, ob ? s[7].y : f5.y};
-    o[7] = f2{oa ? s[5].x : f7.x, ob ? s[5].y : f7.y};
-    o[6] = f2{oa ? s[8].x : f6.x, ob ? s[8].y : f6.y};
-    o[8] = f2{oa ? s[6].x : f8.x, ob ? s[6].y : f8.y};
-    return f2{oa ? 0.f : sqrt_cr(usq.x), ob ? 0.f : sqrt_cr(usq.y)};
-}
 
 __device__ __forceinline__ float stream2_accel(const StreamArgs &a, int y) {
     int g = a.gy0 + y;

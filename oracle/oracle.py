@@ -121,11 +121,22 @@ def step_ghosted(params, ghosted: np.ndarray, obst: np.ndarray, accel_row: int):
     return out, float(np.float32(tot))
 
 
-def run(params, obst: np.ndarray, iters: int | None = None, cells: np.ndarray | None = None):
-    """Accelerate once, then `iters` steps. Returns (final_cells, av_vels[iters])."""
+def run(params, obst: np.ndarray, iters: int | None = None, cells: np.ndarray | None = None,
+        accelerate_first: bool = True):
+    """Accelerate once (unless accelerate_first=False: a continuation run, as
+    lbm_run_steps(..., 0)), then `iters` steps. Returns (final_cells, av_vels[iters])."""
     iters = int(params.max_iters if iters is None else iters)
     if cells is None:
         cells = init_cells(params)
+    if not accelerate_first:
+        ob = np.ascontiguousarray(obst, np.uint8)
+        fc = np.float32(free_cells(params, ob))
+        cur = np.ascontiguousarray(cells, dtype=np.float32).copy()
+        av = np.zeros(iters, np.float32)
+        for t in range(iters):
+            cur, tot = step(params, cur, ob)
+            av[t] = np.float32(tot) / fc
+        return cur, av
     cells = np.ascontiguousarray(cells, dtype=np.float32).copy()
     av = np.zeros(max(iters, 1), np.float32)
     rc = lib().oracle_run(ctypes.byref(_p(params)), _f(cells), _u8(np.ascontiguousarray(obst, np.uint8)),

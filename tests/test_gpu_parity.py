@@ -30,12 +30,16 @@ def sha(cells):
 
 
 MODES = ["scalar", "vec4", "step2", "stream2", "stream3", "stream4"]
+# single-domain modes: the lattice-resident persistent kernel serves one sub-domain only
+SINGLE_MODES = MODES + ["resident"]
 
 
 def mode_kw(native, mode):
     """Engine options selecting one step kernel."""
     if mode.startswith("stream"):
         return dict(kernel=native.KERNEL_STREAM, steps_per_launch=int(mode[6:]))
+    if mode == "resident":
+        return dict(kernel=native.KERNEL_RESIDENT)
     return {"scalar": dict(kernel=native.KERNEL_SCALAR, flags=native.FLAG_ONE_STEP),
             "vec4": dict(kernel=native.KERNEL_VEC4, flags=native.FLAG_ONE_STEP),
             "step2": dict(kernel=native.KERNEL_STEP2)}[mode]
@@ -100,7 +104,7 @@ def test_periodic_streaming_gpu(gpu_lib, nx, ny):
 
 # ------------------------------------------------------ small vectors ----
 
-@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("mode", SINGLE_MODES)
 def test_small_vectors_bitwise(gpu_lib, mode):
     ran = 0
     for name, (p, obst, cells0, after) in small_problems().items():
@@ -153,7 +157,7 @@ def test_decomposed_small_ragged(gpu_lib, parts, mode):
 # ------------------------------------------------ reference grids ----
 
 @pytest.mark.parametrize("grid", GRIDS)
-@pytest.mark.parametrize("mode", ["vec4", "step2", "stream4"])
+@pytest.mark.parametrize("mode", ["vec4", "step2", "stream4", "resident"])
 def test_reference_grid_full_run(gpu_lib, grid, mode, tmp_path):
     """Full maxIters run: final lattice bitwise == oracle (sha256), av_vels ~ oracle,
     and the reference gate (check.py, 1 %) against check/*.dat passes."""
@@ -345,3 +349,67 @@ def test_open_periodic_random_bitwise(gpu_lib, mode, version, monkeypatch):
         assert used == kname(mode)
         assert np.array_equal(cells, ref), kw
         np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+# ------------------------------------------------- resident kernel ----
+
+# (version, tile height): v1 scalar 64-column tiles, v2 packed 128-column tiles
+RES_VARIANTS = [(1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 2), (2, 4), (2, 8), (2, 16), (2, 32)]
+
+
+@pytest.mark.parametrize("ver,th", RES_VARIANTS)
+@pytest.mark.parametrize("nx,ny,steps", [(128, 256, 37), (100, 70, 11), (64, 1, 5), (1, 9, 4), (130, 67, 9),
+                                         (2, 5, 6), (256, 3, 7)])
+def test_resident_tiles_bitwise(gpu_lib, ver, th, nx, ny, steps, monkeypatch):
+    """Every resident tile height on exact and ragged tilings (partial last tiles in
+    x and y, one-row and one-column grids): lattice bitwise == oracle."""
+    if ver == 2 and nx % 2:
+        pytest.skip("the packed resident kernel needs an even width")
+    monkeypatch.setenv("LBM_RES_TH", str(th))
+    monkeypatch.setenv("LBM_RES_V", str(ver))
+    p = lio.Params(nx, ny, steps, 10, 0.1, 0.02, 1.7)
+    obst = np.zeros((ny, nx), np.uint8)
+    if ny > 2:
+        obst[0, :] = obst[-1, :] = 1
+    if nx > 4:
+        obst[ny // 3:, nx // 3] = 1
+    rng = np.random.default_rng(nx * 1000 + ny + th)
+    cells0 = (lio.init_cells(p) * (1 + 0.05 * rng.standard_normal((ny, nx, 9)))).astype(np.float32)
+    ref, ref_av = oracle.run(p, obst, steps, cells0)
+    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, steps, kernel=gpu_lib.KERNEL_RESIDENT)
+    assert used == "resident"
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.parametrize("ver", [1, 2])
+def test_resident_1024_runs_continue(gpu_lib, ver, monkeypatch):
+    """1024^2 (BASELINE config 2 grid, 256 co-resident 64x64 tiles): three runs of
+    different lengths continue one state (granule tags keep counting across runs),
+    bitwise == oracle."""
+    monkeypatch.setenv("LBM_RES_V", str(ver))
+    p, obst = load_problem("1024x1024", iters=0)
+    cells0 = lio.init_cells(p)
+    with gpu_lib.Engine(p, obst, kernel=gpu_lib.KERNEL_RESIDENT) as e:
+        assert e.kernel_in_use() == "resident"
+        e.load_cells(cells0)
+        e.run_steps(3, accelerate_first=True)
+        e.run_steps(1)
+        e.run_steps(6)
+        cells, av = e.store(n_av=6)
+    ref = cells0.copy()
+    oracle.accelerate(p, ref, obst)
+    ref, _ = oracle.run(p, obst, 4, ref, accelerate_first=False)
+    ref, ref_av = oracle.run(p, obst, 6, ref, accelerate_first=False)
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-4)
+
+
+def test_resident_rejects_decomposition(gpu_lib):
+    p = lio.Params(128, 128, 4, 10, 0.1, 0.005, 1.85)
+    obst = np.zeros((128, 128), np.uint8)
+    with pytest.raises(gpu_lib.LbmError):
+        gpu_lib.Engine(p, obst, parts=2, devices=[0], kernel=gpu_lib.KERNEL_RESIDENT)
+    with pytest.raises(gpu_lib.LbmError):  # 8192^2 has far more tiles than CUs
+        gpu_lib.Engine(lio.Params(8192, 8192, 4, 10, 0.1, 0.005, 1.85), np.zeros((8192, 8192), np.uint8),
+                       kernel=gpu_lib.KERNEL_RESIDENT)
