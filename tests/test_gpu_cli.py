@@ -28,7 +28,8 @@ def _gate(tmp_path, grid):
                                   ["-n", "1", "--graph-steps", "50"], ["-n", "2", "--device", "loopback",
                                                                       "--kernel", "scalar"],
                                   ["-n", "1", "--kernel", "stream", "--spl", "3"],
-                                  ["-n", "4", "--device", "loopback", "--kernel", "stream"]])
+                                  ["-n", "4", "--device", "loopback", "--kernel", "stream"],
+                                  ["-n", "1", "--kernel", "resident"]])
 def test_lbm_runner_128(gpu_lib, tmp_path, args):
     exe = PKG / "build" / "lbm_runner"
     r = subprocess.run([str(exe), "--params", str(GOLD / "params" / "input_128x128.params"),

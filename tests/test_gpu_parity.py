@@ -326,7 +326,9 @@ def test_stream_size_limits(gpu_lib):
     assert ei.value.code == gpu_lib.LBM_E_INVALID
     with gpu_lib.Engine(p, obst, kernel=gpu_lib.KERNEL_STREAM, steps_per_launch=3) as e:
         assert e.kernel_in_use() == "stream" and e.steps_per_launch() == 3
-    with gpu_lib.Engine(p, obst) as e:
+    with gpu_lib.Engine(p, obst) as e:  # one small sub-domain: AUTO keeps it resident on chip
+        assert e.kernel_in_use() == "resident"
+    with gpu_lib.Engine(p, obst, parts=2, devices=[0]) as e:
         assert e.kernel_in_use() in ("step2", "stream")
 
 
