@@ -147,7 +147,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--tile", default="8192x8192", help="cells per GPU, NXxNY")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "resident", "stream", "step2", "vec4", "scalar"],
+    ap.add_argument("--kernel", default="auto", choices=["auto", "resident", "stream", "step2", "vec4", "scalar", "pipeline"],
                     help="stream: fused S-step register-streaming kernel; step2: fused two-step LDS kernel; "
                          "vec4/scalar: one step per launch; auto: the library's choice")
     ap.add_argument("--spl", type=int, default=0, help="stream: time steps per launch (2..4; 0 = library default)")
@@ -161,7 +161,7 @@ def main() -> int:
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     n = world
-    kernel = {"auto": native.KERNEL_AUTO, "resident": native.KERNEL_RESIDENT, "stream": native.KERNEL_STREAM, "step2": native.KERNEL_STEP2,
+    kernel = {"auto": native.KERNEL_AUTO, "resident": native.KERNEL_RESIDENT, "pipeline": native.KERNEL_PIPELINE, "stream": native.KERNEL_STREAM, "step2": native.KERNEL_STEP2,
               "scalar": native.KERNEL_SCALAR, "vec4": native.KERNEL_VEC4}[args.kernel]
     kflags = native.FLAG_ONE_STEP if args.kernel in ("vec4", "scalar") else 0
 

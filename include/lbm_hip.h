@@ -60,7 +60,12 @@ enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
  * through registers.  RESIDENT: every step of a run in one persistent
  * launch with the lattice held on chip (LDS + registers) -- single
  * sub-domain grids small enough for all of their 64-column tiles to be
- * co-resident (1024x1024 and below on MI355X).  AUTO picks the fastest
+ * co-resident (1024x1024 and below on MI355X).  PIPELINE: the unfused
+ * reference pipeline, one kernel per stage and step (accelerate_flow ->
+ * propagate -> rebound -> textbook BGK collision -> av_velocity,
+ * main/LbmPoplibs.cpp:225-233) with the conditional accelerate at the start
+ * of EVERY step -- for per-stage profiles; its numerics differ from the
+ * fused scheme's in the last bits (both pass the reference gate).  AUTO picks the fastest
  * kernel the sub-domain sizes allow; lbm_kernel_in_use reports the choice.
  * LBM_FLAG_ONE_STEP forces one step per launch. */
 enum {
@@ -69,7 +74,8 @@ enum {
     LBM_KERNEL_VEC4 = 2,
     LBM_KERNEL_STEP2 = 3,
     LBM_KERNEL_STREAM = 4,
-    LBM_KERNEL_RESIDENT = 5
+    LBM_KERNEL_RESIDENT = 5,
+    LBM_KERNEL_PIPELINE = 6
 };
 
 /*
@@ -203,7 +209,7 @@ int64_t lbm_total_free_cells(lbm_handle *h);
 int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *n_out);
 
 /* Which step kernel the handle uses (LBM_KERNEL_RESIDENT, _STREAM, _STEP2,
- * _VEC4 or _SCALAR), and how many time steps one of its launches advances
+ * _VEC4, _SCALAR or _PIPELINE), and how many time steps one of its launches advances
  * (RESIDENT: all steps of a run -- the last run's count, max_iters before
  * the first run). */
 int32_t lbm_kernel_in_use(lbm_handle *h);

@@ -55,6 +55,13 @@ hipError_t launch_soa_to_aos(const float *f, float *aos, long long P, int pitch,
 hipError_t launch_halo_pack(const HaloArgs &a, hipStream_t s);
 hipError_t launch_halo_unpack(const HaloArgs &a, hipStream_t s);
 hipError_t resident_capacity(int variant, int device, int &capacity);
+int pipe_blocks(int w, int h);
+hipError_t launch_pipe_propagate(const float *f, float *t, long long P, int pitch, int w, int h, hipStream_t s);
+hipError_t launch_pipe_rebound(const float *t, float *f, const uint8_t *obst, long long P, int pitch, int w, int h,
+                               hipStream_t s);
+hipError_t launch_pipe_collision(const float *t, float *f, const uint8_t *obst, long long P, int pitch, int w, int h,
+                                 float omega, float *partials, hipStream_t s);
+hipError_t launch_pipe_av(const float *partials, int n, float *av_local, int t, hipStream_t s);
 hipError_t launch_resident(const ResidentArgs &a, int variant, hipStream_t s);
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s);
 }  // namespace lbm
@@ -160,6 +167,7 @@ struct Sub {
     StreamArgs a3_int[2]{}, a3_bnd[2]{};
     int n3_int = 0, n3_bnd = 0;             // stream launch block counts
     int cur = 0;                            // lattice holding the current state
+    float *pipe_partials = nullptr;         // PIPELINE: collision block partials
 };
 
 }  // namespace
@@ -183,6 +191,7 @@ struct lbm_handle {
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
+    bool pipeline = false;   // LBM_KERNEL_PIPELINE: unfused per-stage kernels (lbm_pipeline.hip)
     // lattice-resident persistent kernel (lbm_resident.hip): single sub-domain only
     bool resident = false;
     int res_variant = -1;    // ResVariant (LBM_RES_TH picks the tile height)
@@ -245,7 +254,8 @@ struct lbm_handle {
         resident_max_cells = std::max(0, env_int("LBM_RES_MAX_CELLS", (int)resident_max_cells));
         if (const char *k = getenv("LBM_KERNEL")) {
             const std::string v(k);
-            env_kernel = v == "resident" ? LBM_KERNEL_RESIDENT
+            env_kernel = v == "pipeline" ? LBM_KERNEL_PIPELINE
+                       : v == "resident" ? LBM_KERNEL_RESIDENT
                        : v == "stream" ? LBM_KERNEL_STREAM : v == "step2" ? LBM_KERNEL_STEP2
                        : v == "vec4" ? LBM_KERNEL_VEC4 : v == "scalar" ? LBM_KERNEL_SCALAR : -1;
         }
@@ -642,6 +652,10 @@ struct lbm_handle {
             throw lbm_failure(LBM_E_INVALID,
                               "vec4 kernel needs sub-domain widths that are multiples of 4 (>= 8 when split in x)");
         vec4 = (kernel == LBM_KERNEL_SCALAR) ? false : can_vec;
+        if (kernel == LBM_KERNEL_PIPELINE) {  // per-stage kernels, W1 halo of the pre-propagate lattice
+            pipeline = true;
+            fused = false;
+        }
         if (kernel == LBM_KERNEL_VEC4 || kernel == LBM_KERNEL_SCALAR) {
             if (env_kernel >= 0 && cfg.kernel == LBM_KERNEL_AUTO) fused = false;  // LBM_KERNEL=vec4|scalar: one step per launch
         }
@@ -728,8 +742,13 @@ struct lbm_handle {
             set_device(s);
             build_args(s);
         }
+        if (pipeline)
+            for (auto &s : subs) {
+                set_device(s);
+                HIP_CHECK(hipMalloc(&s.pipe_partials, sizeof(float) * (size_t)round_up(pipe_blocks(s.w, s.h), 4)));
+            }
         // lattice-resident kernel: one sub-domain whose 64-column tiles can all be co-resident
-        const bool res_ok = parts == 1 && !force_exchange && subs.size() == 1;
+        const bool res_ok = parts == 1 && !force_exchange && subs.size() == 1 && !pipeline;
         if (kernel == LBM_KERNEL_RESIDENT && !res_ok)
             throw lbm_failure(LBM_E_INVALID, "resident kernel needs a single sub-domain without forced exchange");
         if (res_ok && (kernel == LBM_KERNEL_RESIDENT ||
@@ -875,6 +894,53 @@ struct lbm_handle {
             throw lbm_failure(LBM_E_INTERNAL, "resident kernel: a neighbour hand-off timed out (tiles not co-resident?)");
         last_seconds = ms * 1e-3;
         last_steps = steps;
+    }
+
+    // Unfused pipeline, one kernel per stage (lbm_pipeline.hip): every step
+    // accelerates row ny-2 (conditionally), refreshes the W1 ghost ring of
+    // the current lattice (exchanging across sub-domains), propagates into
+    // the other lattice, rebounds / collides back, and folds the |u|
+    // partials into av_local[t].  The current lattice never changes parity.
+    void run_pipeline(int steps) {
+        const float w1 = p.density * p.accel / 9.f;
+        const float w2 = p.density * p.accel / 36.f;
+        Sub &s0 = subs[0];
+        set_device(s0);
+        HIP_CHECK(hipEventRecord(t0, s0.s_comp));
+        for (size_t k = 1; k < subs.size(); ++k) {
+            set_device(subs[k]);
+            HIP_CHECK(hipStreamWaitEvent(subs[k].s_comp, t0, 0));
+        }
+        for (int t = 0; t < steps; ++t) {
+            for (auto &s : subs) {
+                if (s.accel_row < 0 || p.ny < 2) continue;
+                set_device(s);
+                HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+            }
+            refresh_halos();
+            for (auto &s : subs) {
+                set_device(s);
+                float *cells = s.o[s.cur], *tmp = s.o[1 - s.cur];
+                HIP_CHECK(launch_pipe_propagate(cells, tmp, s.plane, s.pitch, s.w, s.h, s.s_comp));
+                HIP_CHECK(launch_pipe_rebound(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, s.s_comp));
+                HIP_CHECK(launch_pipe_collision(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, p.omega,
+                                                s.pipe_partials, s.s_comp));
+                HIP_CHECK(launch_pipe_av(s.pipe_partials, pipe_blocks(s.w, s.h), s.av_local, t, s.s_comp));
+            }
+        }
+        for (auto &s : subs) {
+            set_device(s);
+            HIP_CHECK(hipEventRecord(s.ev_end, s.s_comp));
+        }
+        set_device(s0);
+        for (size_t k = 1; k < subs.size(); ++k) HIP_CHECK(hipStreamWaitEvent(s0.s_comp, subs[k].ev_end, 0));
+        HIP_CHECK(hipEventRecord(t1, s0.s_comp));
+        HIP_CHECK(hipEventSynchronize(t1));
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, t0, t1));
+        last_seconds = ms * 1e-3;
+        last_steps = steps;
+        sync_all();
     }
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
@@ -1167,6 +1233,10 @@ struct lbm_handle {
             run_resident(steps, accelerate_first);
             return;
         }
+        if (pipeline) {
+            run_pipeline(steps);
+            return;
+        }
         for (auto &s : subs) {
             set_device(s);
             HIP_CHECK(hipMemsetAsync(s.ctl, 0, 64, s.s_comp));
@@ -1322,6 +1392,7 @@ struct lbm_handle {
                 if (s.partials[k]) (void)hipFree(s.partials[k]);
             }
             if (s.obst) (void)hipFree(s.obst);
+            if (s.pipe_partials) (void)hipFree(s.pipe_partials);
             if (s.obst_g) (void)hipFree(s.obst_g);
             if (s.halo_mem) (void)hipFree(s.halo_mem);
             if (s.av_local) (void)hipFree(s.av_local);
@@ -1486,6 +1557,7 @@ int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *
 int32_t lbm_kernel_in_use(lbm_handle *h) {
     if (!h) return LBM_KERNEL_SCALAR;
     if (h->resident) return LBM_KERNEL_RESIDENT;
+    if (h->pipeline) return LBM_KERNEL_PIPELINE;
     if (h->fused) return h->use_stream ? LBM_KERNEL_STREAM : LBM_KERNEL_STEP2;
     return h->vec4 ? LBM_KERNEL_VEC4 : LBM_KERNEL_SCALAR;
 }

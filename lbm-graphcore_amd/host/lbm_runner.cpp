@@ -2,7 +2,7 @@
 // top of the HIP engine's C ABI instead of a Poplar Engine.
 //
 //   lbm_runner --params P --obstacles O [-n N] [--device gpu|loopback] [-d] [--exe ignored]
-//              [--runs 5] [--kernel auto|resident|stream|step2|vec4|scalar] [--spl S] [--out-dir DIR]
+//              [--runs 5] [--kernel auto|resident|stream|step2|vec4|scalar|pipeline] [--spl S] [--out-dir DIR]
 //
 // Flow (same program numbering as the reference):
 //   load params/obstacles -> initialise cells on host -> create engine
@@ -34,7 +34,8 @@ void usage(const char *exe) {
               << "      --params arg     filename of parameters file\n"
               << "      --obstacles arg  filename of obstacles file\n"
               << "      --runs arg       timed re-runs after the first (default: 5)\n"
-              << "      --kernel arg     auto, resident, stream, step2, vec4 or scalar (default: auto; vec4/scalar = one step per launch)\n"
+              << "      --kernel arg     auto, resident, stream, step2, vec4, scalar or pipeline (default: auto; vec4/scalar = one\n"
+              << "                       step per launch; pipeline = unfused per-stage kernels)\n"
               << "      --spl arg        stream kernel: time steps per launch, 2..4 (default: library choice)\n"
               << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n"
               << "      --graph-steps arg  replay the step loop as hipGraphs of 2*arg launches (0 = library default, <0 = off)\n"
@@ -81,7 +82,7 @@ int main(int argc, char *argv[]) {
             runs = std::atoi(v.c_str());
         } else if (a == "--kernel") {
             if (!next(kernel)) { usage(argv[0]); return EXIT_FAILURE; }
-            if (kernel != "auto" && kernel != "resident" && kernel != "stream" && kernel != "step2" && kernel != "vec4" && kernel != "scalar") {
+            if (kernel != "auto" && kernel != "resident" && kernel != "pipeline" && kernel != "stream" && kernel != "step2" && kernel != "vec4" && kernel != "scalar") {
                 usage(argv[0]);
                 return EXIT_FAILURE;
             }
@@ -176,6 +177,7 @@ int main(int argc, char *argv[]) {
                    : kernel == "step2"  ? LBM_KERNEL_STEP2
                    : kernel == "stream" ? LBM_KERNEL_STREAM
                    : kernel == "resident" ? LBM_KERNEL_RESIDENT
+                   : kernel == "pipeline" ? LBM_KERNEL_PIPELINE
                                         : LBM_KERNEL_AUTO;
         if (kernel == "scalar" || kernel == "vec4") cfg.flags |= LBM_FLAG_ONE_STEP;
         cfg.steps_per_launch = spl;
@@ -191,7 +193,7 @@ int main(int argc, char *argv[]) {
                       << ",col:" << rects[i].x0 << ")" << std::endl;
         const int32_t k = lbm_kernel_in_use(h);
         std::cout << "step kernel: "
-                  << (k == LBM_KERNEL_RESIDENT ? "resident" : k == LBM_KERNEL_STREAM ? "stream" : k == LBM_KERNEL_STEP2 ? "step2" : k == LBM_KERNEL_VEC4 ? "vec4" : "scalar")
+                  << (k == LBM_KERNEL_RESIDENT ? "resident" : k == LBM_KERNEL_PIPELINE ? "pipeline" : k == LBM_KERNEL_STREAM ? "stream" : k == LBM_KERNEL_STEP2 ? "step2" : k == LBM_KERNEL_VEC4 ? "vec4" : "scalar")
                   << " (" << lbm_steps_per_launch(h) << " steps per launch)" << std::endl;
     }
     lbmhost::timedStep("Running copy to device step", [&]() {

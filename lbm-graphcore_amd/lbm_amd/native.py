@@ -24,7 +24,7 @@ ABI_VERSION = 2          # LBM_ABI_VERSION in include/lbm_hip.h
 LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
 TRANSPORT_LOCAL, TRANSPORT_RCCL = 0, 1
-KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4, KERNEL_STEP2, KERNEL_STREAM, KERNEL_RESIDENT = 0, 1, 2, 3, 4, 5
+KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4, KERNEL_STEP2, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PIPELINE = range(7)
 FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP = 1, 2
 
 # every symbol include/lbm_hip.h declares
@@ -246,7 +246,7 @@ class Engine:
 
     def kernel_in_use(self) -> str:
         return {KERNEL_SCALAR: "scalar", KERNEL_VEC4: "vec4", KERNEL_STEP2: "step2", KERNEL_STREAM: "stream",
-                KERNEL_RESIDENT: "resident"}[
+                KERNEL_RESIDENT: "resident", KERNEL_PIPELINE: "pipeline"}[
             int(self._L.lbm_kernel_in_use(self._h))]
 
     def steps_per_launch(self) -> int:

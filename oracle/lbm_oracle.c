@@ -17,6 +17,13 @@
  *   - av_vels[t] = tot_u / free cells main/LastChance.cpp:266, :486-493
  *   - Reynolds number                 main/include/LatticeBoltzmannUtils.hpp:202-205
  *   - av_velocity of a state          main/LastChance.cpp:290-339
+ *   - UNFUSED pipeline: per step accelerate_flow ->
+ *     propagate -> rebound -> collision -> av_velocity as separate passes,
+ *     main/LbmPoplibs.cpp:225-233 + :23-95 (timestep / averageVelocity), the
+ *     conditional accelerate every step (LastChance.cpp:161-183,
+ *     D2Q9CodeletsOld.cpp:52-80), the textbook BGK CollisionVertex
+ *     (main/codelets/D2Q9CodeletsOptimised.cpp:102-212) and
+ *     AppendReducedSum total / count (D2Q9Codelets.cpp:18-38)
  *
  * Parity pin: tests/test_oracle.py checks this restatement against the
  * reference's committed check/*.dat fixtures (copied, gzipped, into
@@ -265,4 +272,104 @@ float oracle_reynolds(const oracle_params *p, float av_velocity)
 {
     const float viscosity = 1.f / 6.f * (2.f / p->omega - 1.f);
     return av_velocity * (float)p->reynolds_dim / viscosity;
+}
+
+/* ---- unfused pipeline (main/LbmPoplibs.cpp timestep + averageVelocity) ---- */
+
+/* propagate: tmp[k](x, y) = cells[k](x - cx_k, y - cy_k), periodic
+ * (LbmPoplibs.cpp:134-175 PropagateVertex with wrap-around halos). */
+void oracle_pipe_propagate(const oracle_params *p, const float *cells, float *tmp)
+{
+    const int nx = p->nx, ny = p->ny;
+    for (int y = 0; y < ny; y++) {
+        const int yn = (y + 1) % ny, ys = (y == 0) ? ny - 1 : y - 1;
+        for (int x = 0; x < nx; x++) {
+            const int xe = (x + 1) % nx, xw = (x == 0) ? nx - 1 : x - 1;
+            float *t = tmp + ((size_t)y * nx + x) * Q;
+#define AT(xx, yy, k) cells[((size_t)(yy) * nx + (xx)) * Q + (k)]
+            t[0] = AT(x, y, 0);
+            t[1] = AT(xw, y, 1);
+            t[2] = AT(x, ys, 2);
+            t[3] = AT(xe, y, 3);
+            t[4] = AT(x, yn, 4);
+            t[5] = AT(xw, ys, 5);
+            t[6] = AT(xe, ys, 6);
+            t[7] = AT(xe, yn, 7);
+            t[8] = AT(xw, yn, 8);
+#undef AT
+        }
+    }
+}
+
+/* rebound on obstacle cells: cells_k = tmp_opp(k) (CollisionVertex rebound
+ * branch, D2Q9CodeletsOptimised.cpp:141-149; speed 0 keeps its value). */
+void oracle_pipe_rebound(const oracle_params *p, const float *tmp, float *cells, const uint8_t *obst)
+{
+    const size_t n = (size_t)p->nx * (size_t)p->ny;
+    for (size_t i = 0; i < n; i++) {
+        if (!obst[i]) continue;
+        const float *s = tmp + i * Q;
+        float *o = cells + i * Q;
+        o[0] = s[0]; o[1] = s[3]; o[2] = s[4]; o[3] = s[1]; o[4] = s[2];
+        o[5] = s[7]; o[6] = s[8]; o[7] = s[5]; o[8] = s[6];
+    }
+}
+
+/* Textbook BGK on fluid cells (D2Q9CodeletsOptimised.cpp:150-205, every
+ * expression in its order): returns the sum of |u| (pre-collision) over the
+ * fluid cells in row-major order; *count receives their number. */
+float oracle_pipe_collision(const oracle_params *p, const float *tmp, float *cells, const uint8_t *obst,
+                            int64_t *count)
+{
+    const float c_sq = 1.f / 3.f;
+    const float cc2 = (2.f * c_sq * c_sq);
+    const float w0 = 4.f / 9.f, w1 = 1.f / 9.f, w2 = 1.f / 36.f;
+    const float o = p->omega;
+    const size_t n = (size_t)p->nx * (size_t)p->ny;
+    float tot = 0.f;
+    int64_t cnt = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (obst[i]) continue;
+        const float *in = tmp + i * Q;
+        float *out = cells + i * Q;
+        float local_density = 0.f;
+        for (int kk = 0; kk < Q; kk++) local_density += in[kk];
+        const float u_x = ((in[1] + in[5] + in[8]) - (in[3] + in[6] + in[7])) / local_density;
+        const float u_y = ((in[2] + in[5] + in[6]) - (in[4] + in[7] + in[8])) / local_density;
+        const float u_sq = u_x * u_x + u_y * u_y;
+        tot += sqrtf(u_sq);
+        cnt++;
+        const float u[Q] = {0, u_x, u_y, -u_x, -u_y, u_x + u_y, -u_x + u_y, -u_x - u_y, u_x - u_y};
+        const float u_over_2csq = u_sq / (2.f * c_sq);
+        float d_equ[Q];
+        d_equ[0] = w0 * local_density * (1.f - u_over_2csq);
+        for (int k = 1; k < Q; k++) {
+            const float wk = k < 5 ? w1 : w2;
+            d_equ[k] = wk * local_density * (1.f + u[k] / c_sq + (u[k] * u[k]) / cc2 - u_over_2csq);
+        }
+        for (int kk = 0; kk < Q; kk++) out[kk] = in[kk] + o * (d_equ[kk] - in[kk]);
+    }
+    if (count) *count = cnt;
+    return tot;
+}
+
+/* accelerate_flow -> propagate -> rebound -> collision -> av_velocity,
+ * `iters` times (LbmPoplibs.cpp:362-365: Repeat(maxIters, {timestep,
+ * averageVelocity}); the accelerate runs at the start of EVERY step).
+ * av_vels[t] = total / count (AppendReducedSum).  Returns 0 or -1. */
+int oracle_pipe_run(const oracle_params *p, float *cells, const uint8_t *obst, int iters, float *av_vels)
+{
+    const size_t n = (size_t)p->nx * (size_t)p->ny * Q;
+    float *tmp = (float *)malloc(n * sizeof(float));
+    if (!tmp) return -1;
+    for (int t = 0; t < iters; t++) {
+        oracle_accelerate(p, cells, obst);
+        oracle_pipe_propagate(p, cells, tmp);
+        oracle_pipe_rebound(p, tmp, cells, obst);
+        int64_t cnt = 0;
+        const float tot = oracle_pipe_collision(p, tmp, cells, obst, &cnt);
+        if (av_vels) av_vels[t] = tot / (float)cnt;
+    }
+    free(tmp);
+    return 0;
 }

@@ -68,6 +68,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_run.restype = ctypes.c_int
         L.oracle_av_velocity.argtypes = [P, f32p, u8p]
         L.oracle_av_velocity.restype = ctypes.c_float
+        L.oracle_pipe_run.argtypes = [P, f32p, u8p, ctypes.c_int, f32p]
+        L.oracle_pipe_run.restype = ctypes.c_int
         L.oracle_reynolds.argtypes = [P, ctypes.c_float]
         L.oracle_reynolds.restype = ctypes.c_float
         _lib = L
@@ -143,6 +145,21 @@ def run(params, obst: np.ndarray, iters: int | None = None, cells: np.ndarray | 
                           iters, _f(av))
     if rc != 0:
         raise MemoryError("oracle_run allocation failed")
+    return cells, av[:iters]
+
+
+def pipe_run(params, obst: np.ndarray, iters: int | None = None, cells: np.ndarray | None = None):
+    """Unfused pipeline (accelerate -> propagate -> rebound -> textbook collision ->
+    av_velocity) `iters` times. Returns (final_cells, av_vels[iters])."""
+    iters = int(params.max_iters if iters is None else iters)
+    if cells is None:
+        cells = init_cells(params)
+    cells = np.ascontiguousarray(cells, dtype=np.float32).copy()
+    av = np.zeros(max(iters, 1), np.float32)
+    rc = lib().oracle_pipe_run(ctypes.byref(_p(params)), _f(cells), _u8(np.ascontiguousarray(obst, np.uint8)),
+                               iters, _f(av))
+    if rc != 0:
+        raise MemoryError("oracle_pipe_run allocation failed")
     return cells, av[:iters]
 
 

@@ -13,6 +13,10 @@ container, where /root/reference exists; the GPU box only reads the output).
   oracle/<grid>.av_vels.npy.gz   oracle av_vels (float32) for every step
   small.npz           full lattices after 1, 2 and 10 steps on small synthetic
                       problems (walls, interior wall, ragged widths, 1-row grid)
+  oracle_pipe/<grid>.json, .av_vels.npy.gz
+                      the same for the UNFUSED pipeline restatement
+                      (oracle_pipe_run: accelerate every step, textbook BGK),
+                      plus its check.py result against the reference fixtures
 
 Usage: python tests/golden/make_golden.py [--grids 128x128,...] [--jobs N]
 """
@@ -98,6 +102,38 @@ def run_grid(grid: str) -> dict:
     return out
 
 
+def run_pipe_grid(grid: str) -> dict:
+    from lbm_amd import check as lcheck
+    pf, of = grid_files(grid)
+    p = lio.Params.from_file(str(pf))
+    obst = lio.read_obstacles(p.nx, p.ny, str(of))
+    cells, av = oracle.pipe_run(p, obst)
+    out = {
+        "grid": grid, "nx": p.nx, "ny": p.ny, "steps": p.max_iters,
+        "final_f_sha256": lattice_sha256(cells),
+        "reynolds_last_av": oracle.reynolds(p, float(av[-1])),
+        "total_density": float(np.sum(cells, dtype=np.float64)),
+    }
+    buf = _io.BytesIO()
+    np.save(buf, av.astype(np.float32))
+    (GOLD / "oracle_pipe" / f"{grid}.av_vels.npy.gz").write_bytes(gzip.compress(buf.getvalue(), 9))
+    with tempfile.TemporaryDirectory() as wd:
+        lio.write_average_velocities(os.path.join(wd, "av.dat"), av)
+        fs_fix = GOLD / "check" / f"{grid}.final_state.dat.gz"
+        if fs_fix.exists():
+            lio.write_results(os.path.join(wd, "fs.dat"), p, obst, cells)
+            res = lcheck.compare(GOLD / "check" / f"{grid}.av_vels.dat.gz", fs_fix, os.path.join(wd, "av.dat"),
+                                 os.path.join(wd, "fs.dat"), 1.0)
+            out["check_py"] = {"passed": res["passed"], "av_max_diff_pcnt": res["av"]["max_diff_pcnt"],
+                               "fs_max_diff_pcnt": res["fs"]["max_diff_pcnt"]}
+        else:
+            d = lcheck.diff_values(lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz"),
+                                   lcheck.load_av_vels(os.path.join(wd, "av.dat")))
+            out["check_py"] = {"passed": abs(d["max_diff_pcnt"]) < 1.0, "av_max_diff_pcnt": d["max_diff_pcnt"]}
+    (GOLD / "oracle_pipe" / f"{grid}.json").write_text(json.dumps(out, indent=1) + "\n")
+    return out
+
+
 def small_problems():
     """Small synthetic problems for step-level bitwise vectors."""
     probs = []
@@ -158,6 +194,7 @@ def main():
     ap.add_argument("--grids", default=",".join(GRIDS))
     ap.add_argument("--jobs", type=int, default=4)
     ap.add_argument("--skip-small", action="store_true")
+    ap.add_argument("--pipe-grids", default="", help="also write oracle_pipe/ manifests for these grids")
     a = ap.parse_args()
     oracle.build()
     (GOLD / "oracle").mkdir(exist_ok=True)
@@ -165,8 +202,12 @@ def main():
         make_small()
         print("small.npz written")
     grids = [g for g in a.grids.split(",") if g]
+    pipe = [g for g in a.pipe_grids.split(",") if g]
+    (GOLD / "oracle_pipe").mkdir(exist_ok=True)
     with ProcessPoolExecutor(max_workers=a.jobs) as ex:
         for res in ex.map(run_grid, grids):
+            print(json.dumps(res))
+        for res in ex.map(run_pipe_grid, pipe):
             print(json.dumps(res))
 
 

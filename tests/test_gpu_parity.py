@@ -7,7 +7,10 @@ gate (check.py semantics, 1 %) passes on all four reference grids.
 """
 from __future__ import annotations
 
+import gzip
 import hashlib
+import io
+import json
 
 import numpy as np
 import pytest
@@ -415,3 +418,56 @@ def test_resident_rejects_decomposition(gpu_lib):
     with pytest.raises(gpu_lib.LbmError):  # 8192^2 has far more tiles than CUs
         gpu_lib.Engine(lio.Params(8192, 8192, 4, 10, 0.1, 0.005, 1.85), np.zeros((8192, 8192), np.uint8),
                        kernel=gpu_lib.KERNEL_RESIDENT)
+
+
+# ------------------------------------------------ unfused pipeline ----
+# accelerate_flow -> propagate -> rebound -> textbook collision -> av_velocity,
+# one kernel per stage (LbmPoplibs.cpp:225-233); parity vs oracle_pipe_run.
+
+def pipe_manifest(grid):
+    return json.loads((GOLD / "oracle_pipe" / f"{grid}.json").read_text())
+
+
+def test_pipeline_small_bitwise(gpu_lib):
+    ran = 0
+    for name, (p, obst, cells0, _) in small_problems().items():
+        for n in (1, 3, 10):
+            ref, ref_av = oracle.pipe_run(p, obst, n, cells0)
+            cells, av, used = gpu_run(gpu_lib, p, obst, cells0, n, kernel=gpu_lib.KERNEL_PIPELINE)
+            assert used == "pipeline"
+            assert np.array_equal(cells, ref), (name, n)
+            np.testing.assert_allclose(av, ref_av, rtol=1e-5, err_msg=name)
+            ran += 1
+    assert ran > 0
+
+
+@pytest.mark.parametrize("parts,grid", [(2, (1, 2)), (2, (2, 1)), (4, (2, 2)), (6, (3, 2))])
+def test_pipeline_decomposed_bitwise(gpu_lib, parts, grid):
+    """Sub-domains on GPU 0 exchanging the W1 halo before every propagate."""
+    p, obst = load_problem("128x256", iters=23)
+    cells0 = lio.init_cells(p)
+    ref, ref_av = oracle.pipe_run(p, obst, 23, cells0)
+    cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 23, parts=parts, grid=grid, devices=[0],
+                              kernel=gpu_lib.KERNEL_PIPELINE)
+    assert used == "pipeline"
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.parametrize("grid", ["128x128", "128x256", "256x256"])
+def test_pipeline_reference_grid_full_run(gpu_lib, grid, tmp_path):
+    """Full maxIters: final lattice sha256 == the pipeline oracle's, av_vels ~ oracle,
+    and the reference gate (check.py vs check/*.dat) passes."""
+    p, obst = load_problem(grid)
+    m = pipe_manifest(grid)
+    with gpu_lib.Engine(p, obst, kernel=gpu_lib.KERNEL_PIPELINE) as e:
+        e.load_cells(lio.init_cells(p))
+        e.run()
+        cells, av = e.store()
+    assert sha(cells) == m["final_f_sha256"]
+    ref_av = np.load(io.BytesIO(gzip.decompress((GOLD / "oracle_pipe" / f"{grid}.av_vels.npy.gz").read_bytes())))
+    np.testing.assert_allclose(av, ref_av, rtol=AV_RTOL)
+    lio.write_average_velocities(str(tmp_path / "av_vels.dat"), av)
+    d = lcheck.diff_values(lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz"),
+                           lcheck.load_av_vels(tmp_path / "av_vels.dat"))
+    assert abs(d["max_diff_pcnt"]) < 1.0
