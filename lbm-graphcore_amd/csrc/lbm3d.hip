@@ -1,0 +1,747 @@
+// lbm3d.hip -- D3Q19-BGK engine (include/lbm3d_hip.h): BASELINE config 5,
+// SURVEY 8f rank 4.  The reference has no 3-D code; this is the 3-D analogue
+// of its fused D2Q9 step (main/LastChance.cpp:192-266) on the same machinery
+// as the D2Q9 engine: SoA lattice pair, one fused pull-stream / bounce-back /
+// BGK / body-force / |u| kernel, device-side per-step |u| partials, slab
+// decomposition with halos over RCCL (or device copies), boundary planes on a
+// high-priority stream so the exchange overlaps the interior.
+//
+// Layout per slab of nzs planes: f[z + 1][k][y][px] for -1 <= z <= nzs (one
+// ghost plane below and above); speeds ordered so that the five that cross
+// the top face (c_z = +1: 9..13) and the five that cross the bottom face
+// (c_z = -1: 14..18) are each ONE contiguous block of a plane -- the halo
+// message of a face is a single contiguous range of the lattice, sent and
+// received in place (no pack / unpack kernels).  x and y wrap in-kernel.
+//
+// Bandwidth-bound: 152 algorithmic bytes per cell update (19 fp32 loads + 19
+// stores); no MFMA.  Arithmetic in IEEE fp32 evaluated in the order of
+// oracle/lbm_oracle3d.c (-ffp-contract=off, correctly rounded / and sqrt), so
+// the lattice is bitwise equal to the CPU restatement.
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "lbm3d_hip.h"
+#include "lbm_device.hpp"
+
+namespace lbm {
+
+constexpr int Q3 = 19;
+constexpr int B3X = 64, B3Y = 4;  // block: 64 x-columns (one wave) x 4 rows
+
+struct Step3Args {
+    const float *fin;        // origin (plane z = 0) of the lattice read
+    float *fout;             // origin of the lattice written
+    const uint8_t *obst;     // [nzs][ny][nx]
+    long long PL, KS;        // plane stride, speed stride (floats)
+    int px, nx, ny;
+    int z0;                  // first plane of this launch
+    float omega, omo, w1, w2;
+    float *partials;         // this launch writes partials[block]
+};
+
+__global__ __launch_bounds__(B3X * B3Y) void step3d(Step3Args a) {
+    __shared__ float lds[B3X * B3Y / 64];
+    const int x = blockIdx.x * B3X + threadIdx.x;
+    const int y = blockIdx.y * B3Y + threadIdx.y;
+    const int z = a.z0 + blockIdx.z;
+    float usum = 0.f;
+    if (x < a.nx && y < a.ny) {
+        const int xw = x == 0 ? a.nx - 1 : x - 1, xe = x == a.nx - 1 ? 0 : x + 1;
+        const int ys = y == 0 ? a.ny - 1 : y - 1, yn = y == a.ny - 1 ? 0 : y + 1;
+        const long long PL = a.PL, KS = a.KS;
+        const int px = a.px;
+        // pulled populations s_k = f_k(x - cx, y - cy, z - cz)
+        const float *p0 = a.fin + (long long)z * PL;  // plane z
+        const float *pm = p0 - PL;                     // plane z-1 (c_z = +1 pulls from below)
+        const float *pp = p0 + PL;                     // plane z+1
+        const long long ry = (long long)y * px, rs = (long long)ys * px, rn = (long long)yn * px;
+        float s[Q3];
+        s[0] = p0[0 * KS + ry + x];
+        s[1] = p0[1 * KS + ry + xw];
+        s[2] = p0[2 * KS + ry + xe];
+        s[3] = p0[3 * KS + rs + x];
+        s[4] = p0[4 * KS + rn + x];
+        s[5] = p0[5 * KS + rs + xw];
+        s[6] = p0[6 * KS + rn + xe];
+        s[7] = p0[7 * KS + rn + xw];
+        s[8] = p0[8 * KS + rs + xe];
+        s[9] = pm[9 * KS + ry + x];
+        s[10] = pm[10 * KS + ry + xw];
+        s[11] = pm[11 * KS + ry + xe];
+        s[12] = pm[12 * KS + rs + x];
+        s[13] = pm[13 * KS + rn + x];
+        s[14] = pp[14 * KS + ry + x];
+        s[15] = pp[15 * KS + ry + xe];
+        s[16] = pp[16 * KS + ry + xw];
+        s[17] = pp[17 * KS + rn + x];
+        s[18] = pp[18 * KS + rs + x];
+        float o[Q3];
+        const bool ob = a.obst[((long long)blockIdx.z * a.ny + y) * a.nx + x] != 0;
+        if (ob) {  // bounce-back: out_k = s_opp(k)
+            o[0] = s[0];
+            o[1] = s[2];
+            o[2] = s[1];
+            o[3] = s[4];
+            o[4] = s[3];
+            o[5] = s[6];
+            o[6] = s[5];
+            o[7] = s[8];
+            o[8] = s[7];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                o[9 + i] = s[14 + i];
+                o[14 + i] = s[9 + i];
+            }
+        } else {
+            const float rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8] + s[9] + s[10] + s[11] +
+                              s[12] + s[13] + s[14] + s[15] + s[16] + s[17] + s[18];
+            const float ux = ((s[1] + s[5] + s[7] + s[10] + s[16]) - (s[2] + s[6] + s[8] + s[11] + s[15])) / rho;
+            const float uy = ((s[3] + s[5] + s[8] + s[12] + s[18]) - (s[4] + s[6] + s[7] + s[13] + s[17])) / rho;
+            const float uz = ((s[9] + s[10] + s[11] + s[12] + s[13]) - (s[14] + s[15] + s[16] + s[17] + s[18])) / rho;
+            const float usq = ux * ux + uy * uy + uz * uz;
+            const float c = 1.00f - usq * 1.50f;
+            const float ld0 = rho / 3.00f * a.omega;
+            const float ld1 = rho / 18.00f * a.omega;
+            const float ld2 = rho / 36.00f * a.omega;
+            const float pxy = ux + uy, mxy = ux - uy, pxz = ux + uz, mxz = -ux + uz, pyz = uy + uz, myz = -uy + uz;
+            const float e[Q3] = {0.f, ux, -ux, uy, -uy, pxy, -pxy, mxy, -mxy, uz, pxz, mxz, pyz, myz,
+                                 -uz, -pxz, -mxz, -pyz, -myz};
+            const float omo = a.omo;
+            o[0] = s[0] * omo + ld0 * c;
+#pragma unroll
+            for (int k = 1; k < Q3; ++k) {
+                const float ld = (k <= 4 || k == 9 || k == 14) ? ld1 : ld2;
+                o[k] = s[k] * omo + ld * ((4.50f * e[k]) * (2.00f / 3.00f + e[k]) + c);
+            }
+            const float w1 = a.w1, w2 = a.w2;
+            o[1] = o[1] + w1;
+            o[2] = o[2] - w1;
+            o[5] = o[5] + w2;
+            o[6] = o[6] - w2;
+            o[7] = o[7] + w2;
+            o[8] = o[8] - w2;
+            o[10] = o[10] + w2;
+            o[11] = o[11] - w2;
+            o[15] = o[15] - w2;
+            o[16] = o[16] + w2;
+            usum = sqrtf(usq);
+        }
+        float *d = a.fout + (long long)z * PL + ry + x;
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) d[k * KS] = o[k];
+    }
+    // block partial in a fixed order (waves in threadIdx order)
+    float v = usum;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    const int t = threadIdx.y * B3X + threadIdx.x;
+    if ((t & 63) == 0) lds[t >> 6] = v;
+    __syncthreads();
+    if (t == 0) {
+        float b = lds[0];
+#pragma unroll
+        for (int i = 1; i < B3X * B3Y / 64; ++i) b += lds[i];
+        a.partials[((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = b;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void reduce3d(const float *partials, int n, float *av_local, int t) {
+    __shared__ float lds[BLOCK / 64];
+    const float v = sum_partials_n<BLOCK>(partials, n, lds);
+    if (threadIdx.x == 0) av_local[t] = v;
+}
+
+// every plane (ghosts included) at rest equilibrium
+__global__ __launch_bounds__(BLOCK) void init3d(float *base, long long planes, long long KS, long long PL, float c0,
+                                               float c1, float c2) {
+    const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= planes * KS) return;
+    const long long z = i / KS, r = i - z * KS;
+    float *d = base + z * PL + r;
+    d[0] = c0;
+#pragma unroll
+    for (int k = 1; k < Q3; ++k) d[k * KS] = (k <= 4 || k == 9 || k == 14) ? c1 : c2;
+}
+
+// AoS [nzs][ny][nx][19] staging <-> lattice interior
+__global__ __launch_bounds__(BLOCK) void aos_to_soa3d(const float *aos, float *f, long long PL, long long KS, int px,
+                                                     int nx, int ny, long long n) {
+    const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const long long zy = i / nx;
+    const int x = (int)(i - zy * nx);
+    const int y = (int)(zy % ny);
+    const long long z = zy / ny;
+    float *d = f + z * PL + (long long)y * px + x;
+#pragma unroll
+    for (int k = 0; k < Q3; ++k) d[k * KS] = aos[i * Q3 + k];
+}
+
+__global__ __launch_bounds__(BLOCK) void soa_to_aos3d(const float *f, float *aos, long long PL, long long KS, int px,
+                                                     int nx, int ny, long long n) {
+    const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const long long zy = i / nx;
+    const int x = (int)(i - zy * nx);
+    const int y = (int)(zy % ny);
+    const long long z = zy / ny;
+    const float *s = f + z * PL + (long long)y * px + x;
+#pragma unroll
+    for (int k = 0; k < Q3; ++k) aos[i * Q3 + k] = s[k * KS];
+}
+
+}  // namespace lbm
+
+using namespace lbm;
+
+namespace {
+
+struct fail3 : std::runtime_error {
+    int code;
+    fail3(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define H3(expr)                                                                                          \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess) throw fail3(LBM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define N3(expr)                                                                                          \
+    do {                                                                                                  \
+        ncclResult_t r_ = (expr);                                                                         \
+        if (r_ != ncclSuccess) throw fail3(LBM_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+struct Slab {
+    int id = 0, dev = 0, z0 = 0, nzs = 0;
+    float *f[2] = {nullptr, nullptr};  // allocations (ghost plane below first)
+    float *o[2] = {nullptr, nullptr};  // origins: plane z = 0
+    uint8_t *obst = nullptr;
+    float *partials = nullptr;
+    int nblk_all = 0, nblk_bnd = 0, nblk_int = 0;
+    float *av_local = nullptr;
+    int av_cap = 0;
+    int cur = 0;
+    hipStream_t s_comp = nullptr, s_bnd = nullptr, s_comm = nullptr;
+    hipEvent_t ev_b = nullptr, ev_i = nullptr, ev_x = nullptr, ev_end = nullptr;
+};
+
+}  // namespace
+
+struct lbm3d_handle {
+    lbm3d_params p{};
+    int parts = 1, transport = LBM_TRANSPORT_LOCAL, rank = 0, world = 1;
+    int px = 0;
+    long long KS = 0, PL = 0;
+    std::vector<Slab> slabs;
+    std::vector<int> all_z0, all_nz;
+    ncclComm_t comm = nullptr;
+    int64_t free_cells = 0;
+    bool loaded = false;
+    int last_steps = 0;
+    double last_seconds = 0.0;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    std::string err;
+
+    // several slabs, or RCCL transport (then even one rank sends its faces to
+    // itself through RCCL: the exchange path is testable on one GPU)
+    bool multi() const { return parts > 1 || transport == LBM_TRANSPORT_RCCL; }
+    float w1() const { return p.density * p.accel / 18.f; }
+    float w2() const { return p.density * p.accel / 36.f; }
+
+    void create(const lbm3d_params *prm, const uint8_t *obstacles, const lbm_config &cfg) {
+        p = *prm;
+        if (p.nx <= 0 || p.ny <= 0 || p.nz <= 0 || p.max_iters < 0)
+            throw fail3(LBM_E_INVALID, "nx, ny, nz must be > 0 and max_iters >= 0");
+        if (!obstacles) throw fail3(LBM_E_INVALID, "obstacles must not be NULL");
+        parts = cfg.parts > 0 ? cfg.parts : 1;
+        transport = cfg.transport;
+        if (parts > p.nz) throw fail3(LBM_E_INVALID, "more z slabs than planes");
+        int ndev = 0;
+        H3(hipGetDeviceCount(&ndev));
+        if (ndev <= 0) throw fail3(LBM_E_HIP, "no HIP device visible");
+        const long long cells = (long long)p.nx * p.ny * p.nz;
+        free_cells = 0;
+        for (long long i = 0; i < cells; ++i) free_cells += obstacles[i] ? 0 : 1;
+        px = (p.nx + 15) / 16 * 16;  // 64-byte rows
+        KS = (long long)p.ny * px;
+        PL = (long long)Q3 * KS;
+        // round-robin z extents (StructuredGridUtils.hpp:161-165 rule, in z)
+        all_z0.assign(parts, 0);
+        all_nz.assign(parts, p.nz / parts);
+        for (int i = 0; i < p.nz % parts; ++i) all_nz[i]++;
+        for (int i = 1; i < parts; ++i) all_z0[i] = all_z0[i - 1] + all_nz[i - 1];
+        std::vector<int> mine;
+        if (transport == LBM_TRANSPORT_RCCL) {
+            if (cfg.world != parts || cfg.rank < 0 || cfg.rank >= parts)
+                throw fail3(LBM_E_INVALID, "RCCL transport needs world == parts and 0 <= rank < world");
+            if (!cfg.rccl_unique_id) throw fail3(LBM_E_INVALID, "RCCL transport needs rccl_unique_id");
+            rank = cfg.rank;
+            world = cfg.world;
+            mine.push_back(rank);
+        } else if (transport == LBM_TRANSPORT_LOCAL) {
+            for (int i = 0; i < parts; ++i) mine.push_back(i);
+        } else {
+            throw fail3(LBM_E_INVALID, "unknown transport");
+        }
+        slabs.resize(mine.size());
+        for (size_t k = 0; k < mine.size(); ++k) {
+            Slab &s = slabs[k];
+            s.id = mine[k];
+            s.z0 = all_z0[s.id];
+            s.nzs = all_nz[s.id];
+            if (transport == LBM_TRANSPORT_RCCL)
+                s.dev = (cfg.devices && cfg.num_devices > 0) ? cfg.devices[0] : rank % ndev;
+            else
+                s.dev = (cfg.devices && cfg.num_devices > 0) ? cfg.devices[s.id % cfg.num_devices] : s.id % ndev;
+            if (s.dev < 0 || s.dev >= ndev) throw fail3(LBM_E_INVALID, "device index out of range");
+            alloc(s, obstacles);
+        }
+        if (transport == LBM_TRANSPORT_RCCL) {
+            ncclUniqueId id;
+            memcpy(&id, cfg.rccl_unique_id, sizeof(id));
+            H3(hipSetDevice(slabs[0].dev));
+            N3(ncclCommInitRank(&comm, world, id, rank));
+        } else if (slabs.size() > 1) {
+            for (auto &a : slabs)
+                for (auto &b : slabs)
+                    if (a.dev != b.dev) {
+                        int can = 0;
+                        H3(hipDeviceCanAccessPeer(&can, a.dev, b.dev));
+                        if (can) {
+                            H3(hipSetDevice(a.dev));
+                            hipError_t e = hipDeviceEnablePeerAccess(b.dev, 0);
+                            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) H3(e);
+                            (void)hipGetLastError();
+                        }
+                    }
+        }
+        ensure_av(std::max(p.max_iters, 1));
+        H3(hipSetDevice(slabs[0].dev));
+        H3(hipEventCreate(&t0));
+        H3(hipEventCreate(&t1));
+    }
+
+    int blocks_for(int planes) const {
+        return ((p.nx + B3X - 1) / B3X) * ((p.ny + B3Y - 1) / B3Y) * std::max(planes, 0);
+    }
+
+    void alloc(Slab &s, const uint8_t *obstacles) {
+        H3(hipSetDevice(s.dev));
+        const size_t floats = (size_t)(s.nzs + 2) * PL;
+        for (int k = 0; k < 2; ++k) {
+            H3(hipMalloc(&s.f[k], floats * sizeof(float)));
+            H3(hipMemset(s.f[k], 0, floats * sizeof(float)));
+            s.o[k] = s.f[k] + PL;
+        }
+        const size_t ob = (size_t)s.nzs * p.ny * p.nx;
+        H3(hipMalloc(&s.obst, ob + 256));
+        H3(hipMemcpy(s.obst, obstacles + (size_t)s.z0 * p.ny * p.nx, ob, hipMemcpyHostToDevice));
+        s.nblk_all = blocks_for(s.nzs);
+        s.nblk_bnd = multi() ? blocks_for(s.nzs >= 2 ? 2 : 1) : 0;
+        s.nblk_int = multi() ? blocks_for(s.nzs - 2) : 0;
+        H3(hipMalloc(&s.partials, sizeof(float) * (size_t)(s.nblk_all + 64)));
+        H3(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
+        H3(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
+        int lo = 0, hi = 0;
+        H3(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        H3(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, hi));
+        for (hipEvent_t *e : {&s.ev_b, &s.ev_i, &s.ev_x, &s.ev_end}) H3(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+
+    void ensure_av(int n) {
+        for (auto &s : slabs) {
+            if (s.av_cap >= n) continue;
+            H3(hipSetDevice(s.dev));
+            if (s.av_local) H3(hipFree(s.av_local));
+            s.av_cap = std::max(n, 1);
+            H3(hipMalloc(&s.av_local, sizeof(float) * (size_t)s.av_cap));
+            H3(hipMemset(s.av_local, 0, sizeof(float) * (size_t)s.av_cap));
+        }
+    }
+
+    Slab *local(int id) {
+        for (auto &s : slabs)
+            if (s.id == id) return &s;
+        return nullptr;
+    }
+
+    // one contiguous face block: speeds 9..13 of the top plane (goes up) or
+    // 14..18 of the bottom plane (goes down); ghost targets likewise
+    float *up_src(const Slab &s, int l) const { return s.o[l] + (long long)(s.nzs - 1) * PL + 9 * KS; }
+    float *down_src(const Slab &s, int l) const { return s.o[l] + 14 * KS; }
+    float *below_ghost(const Slab &s, int l) const { return s.o[l] - PL + 9 * KS; }
+    float *above_ghost(const Slab &s, int l) const { return s.o[l] + (long long)s.nzs * PL + 14 * KS; }
+
+    // Fill the ghost planes of lattice l of every slab (on `st` of each slab,
+    // after event `after` of the source slabs).  Single slab: periodic self copies.
+    void exchange(int l, bool use_comm) {
+        const size_t bytes = sizeof(float) * 5 * (size_t)KS;
+        if (!multi()) {
+            Slab &s = slabs[0];
+            H3(hipSetDevice(s.dev));
+            H3(hipMemcpyAsync(below_ghost(s, l), up_src(s, l), bytes, hipMemcpyDeviceToDevice, s.s_comp));
+            H3(hipMemcpyAsync(above_ghost(s, l), down_src(s, l), bytes, hipMemcpyDeviceToDevice, s.s_comp));
+            return;
+        }
+        if (transport == LBM_TRANSPORT_RCCL) {
+            Slab &s = slabs[0];
+            H3(hipSetDevice(s.dev));
+            hipStream_t st = use_comm ? s.s_comm : s.s_comp;
+            H3(hipStreamWaitEvent(st, s.ev_b, 0));
+            const int up = (rank + 1) % world, down = (rank + world - 1) % world;
+            N3(ncclGroupStart());
+            // same posting order on every rank: send up, send down, recv from below, recv from above
+            N3(ncclSend(up_src(s, l), 5 * (size_t)KS, ncclFloat, up, comm, st));
+            N3(ncclSend(down_src(s, l), 5 * (size_t)KS, ncclFloat, down, comm, st));
+            N3(ncclRecv(below_ghost(s, l), 5 * (size_t)KS, ncclFloat, down, comm, st));
+            N3(ncclRecv(above_ghost(s, l), 5 * (size_t)KS, ncclFloat, up, comm, st));
+            N3(ncclGroupEnd());
+            H3(hipEventRecord(s.ev_x, st));
+            return;
+        }
+        for (auto &s : slabs) {  // LOCAL: each slab pulls its two ghost blocks
+            H3(hipSetDevice(s.dev));
+            hipStream_t st = use_comm ? s.s_comm : s.s_comp;
+            Slab *below = local((s.id + parts - 1) % parts), *above = local((s.id + 1) % parts);
+            H3(hipStreamWaitEvent(st, below->ev_b, 0));
+            H3(hipStreamWaitEvent(st, above->ev_b, 0));
+            if (below->dev == s.dev)
+                H3(hipMemcpyAsync(below_ghost(s, l), up_src(*below, l), bytes, hipMemcpyDeviceToDevice, st));
+            else
+                H3(hipMemcpyPeerAsync(below_ghost(s, l), s.dev, up_src(*below, l), below->dev, bytes, st));
+            if (above->dev == s.dev)
+                H3(hipMemcpyAsync(above_ghost(s, l), down_src(*above, l), bytes, hipMemcpyDeviceToDevice, st));
+            else
+                H3(hipMemcpyPeerAsync(above_ghost(s, l), s.dev, down_src(*above, l), above->dev, bytes, st));
+            H3(hipEventRecord(s.ev_x, st));
+        }
+    }
+
+    // st waits for this slab's last exchange and (LOCAL) its neighbours' (they read our faces)
+    void wait_x(Slab &s, hipStream_t st) {
+        H3(hipStreamWaitEvent(st, s.ev_x, 0));
+        if (transport == LBM_TRANSPORT_LOCAL && multi()) {
+            H3(hipStreamWaitEvent(st, local((s.id + parts - 1) % parts)->ev_x, 0));
+            H3(hipStreamWaitEvent(st, local((s.id + 1) % parts)->ev_x, 0));
+        }
+    }
+
+    void launch(Slab &s, int zfirst, int planes, float *partials, hipStream_t st) {
+        if (planes <= 0) return;
+        Step3Args a{};
+        a.fin = s.o[s.cur];
+        a.fout = s.o[1 - s.cur];
+        a.obst = s.obst + (size_t)zfirst * p.ny * p.nx;
+        a.PL = PL;
+        a.KS = KS;
+        a.px = px;
+        a.nx = p.nx;
+        a.ny = p.ny;
+        a.z0 = zfirst;
+        a.omega = p.omega;
+        a.omo = 1 - p.omega;
+        a.w1 = w1();
+        a.w2 = w2();
+        a.partials = partials;
+        dim3 grid((p.nx + B3X - 1) / B3X, (p.ny + B3Y - 1) / B3Y, planes);
+        hipLaunchKernelGGL(step3d, grid, dim3(B3X, B3Y), 0, st, a);
+        H3(hipGetLastError());
+    }
+
+    // one step of every slab: reads lattice cur, writes 1 - cur and its ghosts
+    void step_once(int t) {
+        if (!multi()) {
+            Slab &s = slabs[0];
+            launch(s, 0, s.nzs, s.partials, s.s_comp);
+            exchange(1 - s.cur, false);
+            hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials, s.nblk_all, s.av_local, t);
+            H3(hipGetLastError());
+            s.cur ^= 1;
+            return;
+        }
+        // B(t): faces, after I(t-1) and the exchanges that filled / read our ghosts and faces
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            H3(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
+            wait_x(s, s.s_bnd);
+            launch(s, 0, 1, s.partials, s.s_bnd);
+            if (s.nzs >= 2) launch(s, s.nzs - 1, 1, s.partials + blocks_for(1), s.s_bnd);
+            H3(hipEventRecord(s.ev_b, s.s_bnd));
+        }
+        // X(t): faces of the new lattice -> neighbours' ghost planes, on the comm streams
+        exchange(1 - slabs[0].cur, true);
+        // I(t): interior planes, after B(t) (reduction needs its partials; the
+        // interior reads the faces B(t-1) wrote, already ordered by ev_b)
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            launch(s, 1, s.nzs - 2, s.partials + s.nblk_bnd, s.s_comp);
+            H3(hipStreamWaitEvent(s.s_comp, s.ev_b, 0));
+            hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials, s.nblk_all, s.av_local, t);
+            H3(hipGetLastError());
+            H3(hipEventRecord(s.ev_i, s.s_comp));
+            s.cur ^= 1;
+        }
+    }
+
+    void sync_all() {
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            H3(hipStreamSynchronize(s.s_comp));
+            H3(hipStreamSynchronize(s.s_bnd));
+            H3(hipStreamSynchronize(s.s_comm));
+        }
+    }
+
+    // ghost planes of the current lattice, from its faces (after load / init)
+    void refresh() {
+        if (multi()) {
+            for (auto &s : slabs) {
+                H3(hipSetDevice(s.dev));
+                H3(hipEventRecord(s.ev_b, s.s_comp));
+            }
+            exchange(slabs[0].cur, false);
+        } else {
+            exchange(slabs[0].cur, false);
+        }
+        sync_all();
+    }
+
+    void run_steps(int steps) {
+        if (!loaded) throw fail3(LBM_E_STATE, "lattice not initialised (lbm3d_load_cells / lbm3d_init_equilibrium)");
+        if (steps < 0) throw fail3(LBM_E_INVALID, "steps must be >= 0");
+        ensure_av(std::max(steps, 1));
+        sync_all();
+        Slab &s0 = slabs[0];
+        H3(hipSetDevice(s0.dev));
+        H3(hipEventRecord(t0, s0.s_comp));
+        for (auto &s : slabs) {  // every stream starts after t0 and the last refresh
+            H3(hipSetDevice(s.dev));
+            H3(hipStreamWaitEvent(s.s_comp, t0, 0));
+            H3(hipEventRecord(s.ev_i, s.s_comp));
+            H3(hipEventRecord(s.ev_x, s.s_comp));
+        }
+        for (int t = 0; t < steps; ++t) step_once(t);
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            H3(hipStreamWaitEvent(s.s_comp, s.ev_x, 0));
+            H3(hipEventRecord(s.ev_end, s.s_comp));
+        }
+        H3(hipSetDevice(s0.dev));
+        for (auto &s : slabs) H3(hipStreamWaitEvent(s0.s_comp, s.ev_end, 0));
+        H3(hipEventRecord(t1, s0.s_comp));
+        H3(hipEventSynchronize(t1));
+        float ms = 0.f;
+        H3(hipEventElapsedTime(&ms, t0, t1));
+        last_seconds = ms * 1e-3;
+        last_steps = steps;
+        sync_all();
+    }
+
+    void init_equilibrium() {
+        const float c0 = p.density / 3.f, c1 = p.density / 18.f, c2 = p.density / 36.f;
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            s.cur = 0;
+            const long long planes = s.nzs + 2;
+            hipLaunchKernelGGL(init3d, dim3((unsigned)((planes * KS + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s.s_comp,
+                               s.f[0], planes, KS, PL, c0, c1, c2);
+            H3(hipGetLastError());
+        }
+        sync_all();
+        loaded = true;
+    }
+
+    void load_cells(const float *aos) {
+        if (!aos) throw fail3(LBM_E_INVALID, "cells must not be NULL");
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            const long long n = (long long)s.nzs * p.ny * p.nx;
+            float *stage = nullptr;
+            H3(hipMalloc(&stage, sizeof(float) * Q3 * (size_t)n));
+            H3(hipMemcpy(stage, aos + (size_t)s.z0 * p.ny * p.nx * Q3, sizeof(float) * Q3 * (size_t)n,
+                         hipMemcpyHostToDevice));
+            s.cur = 0;
+            hipLaunchKernelGGL(aos_to_soa3d, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s.s_comp, stage,
+                               s.o[0], PL, KS, px, p.nx, p.ny, n);
+            H3(hipGetLastError());
+            H3(hipStreamSynchronize(s.s_comp));
+            H3(hipFree(stage));
+        }
+        refresh();
+        loaded = true;
+    }
+
+    void store(float *aos, float *av, int n_av) {
+        if (!loaded) throw fail3(LBM_E_STATE, "nothing to store");
+        sync_all();
+        if (aos)
+            for (auto &s : slabs) {
+                H3(hipSetDevice(s.dev));
+                const long long n = (long long)s.nzs * p.ny * p.nx;
+                float *stage = nullptr;
+                H3(hipMalloc(&stage, sizeof(float) * Q3 * (size_t)n));
+                hipLaunchKernelGGL(soa_to_aos3d, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s.s_comp,
+                                   s.o[s.cur], stage, PL, KS, px, p.nx, p.ny, n);
+                H3(hipGetLastError());
+                H3(hipStreamSynchronize(s.s_comp));
+                H3(hipMemcpy(aos + (size_t)s.z0 * p.ny * p.nx * Q3, stage, sizeof(float) * Q3 * (size_t)n,
+                             hipMemcpyDeviceToHost));
+                H3(hipFree(stage));
+            }
+        if (av && n_av > 0) {
+            const int n = std::min(n_av, last_steps);
+            std::vector<float> per((size_t)parts * std::max(n, 1), 0.f);
+            if (n > 0) {
+                if (transport == LBM_TRANSPORT_RCCL) {
+                    Slab &s = slabs[0];
+                    H3(hipSetDevice(s.dev));
+                    float *g = nullptr;
+                    H3(hipMalloc(&g, sizeof(float) * (size_t)n * world));
+                    N3(ncclAllGather(s.av_local, g, (size_t)n, ncclFloat, comm, s.s_comm));
+                    H3(hipStreamSynchronize(s.s_comm));
+                    H3(hipMemcpy(per.data(), g, sizeof(float) * (size_t)n * world, hipMemcpyDeviceToHost));
+                    H3(hipFree(g));
+                } else {
+                    for (auto &s : slabs) {
+                        H3(hipSetDevice(s.dev));
+                        H3(hipMemcpy(per.data() + (size_t)s.id * n, s.av_local, sizeof(float) * (size_t)n,
+                                     hipMemcpyDeviceToHost));
+                    }
+                }
+            }
+            const float fc = (float)free_cells;
+            for (int t = 0; t < n_av; ++t) {
+                if (t >= n) {
+                    av[t] = 0.f;
+                    continue;
+                }
+                float tot = 0.f;
+                for (int r = 0; r < parts; ++r) tot += per[(size_t)r * n + t];  // fixed slab order
+                av[t] = tot / fc;
+            }
+        }
+    }
+
+    void destroy() {
+        for (auto &s : slabs) {
+            if (hipSetDevice(s.dev) != hipSuccess) continue;
+            (void)hipDeviceSynchronize();
+            for (int k = 0; k < 2; ++k)
+                if (s.f[k]) (void)hipFree(s.f[k]);
+            if (s.obst) (void)hipFree(s.obst);
+            if (s.partials) (void)hipFree(s.partials);
+            if (s.av_local) (void)hipFree(s.av_local);
+            for (hipStream_t st : {s.s_comp, s.s_bnd, s.s_comm})
+                if (st) (void)hipStreamDestroy(st);
+            for (hipEvent_t e : {s.ev_b, s.ev_i, s.ev_x, s.ev_end})
+                if (e) (void)hipEventDestroy(e);
+        }
+        if (comm) (void)ncclCommDestroy(comm);
+        if (t0) (void)hipEventDestroy(t0);
+        if (t1) (void)hipEventDestroy(t1);
+    }
+};
+
+namespace {
+thread_local std::string g_err3;
+
+template <class F>
+int guard3(lbm3d_handle *h, F &&f) {
+    try {
+        f();
+        return LBM_OK;
+    } catch (const fail3 &e) {
+        if (h) h->err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        if (h) h->err = "host allocation failed";
+        return LBM_E_NOMEM;
+    } catch (const std::exception &e) {
+        if (h) h->err = e.what();
+        return LBM_E_INTERNAL;
+    } catch (...) {
+        if (h) h->err = "unknown failure";
+        return LBM_E_INTERNAL;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int lbm3d_create(const lbm3d_params *params, const uint8_t *obstacles, const lbm_config *config, lbm3d_handle **out) {
+    if (!params || !out) return LBM_E_INVALID;
+    *out = nullptr;
+    auto *h = new (std::nothrow) lbm3d_handle();
+    if (!h) return LBM_E_NOMEM;
+    lbm_config dflt{};
+    dflt.parts = 1;
+    const int rc = guard3(h, [&] { h->create(params, obstacles, config ? *config : dflt); });
+    if (rc != LBM_OK) {
+        g_err3 = h->err;
+        h->destroy();
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return LBM_OK;
+}
+
+int lbm3d_init_equilibrium(lbm3d_handle *h) {
+    if (!h) return LBM_E_INVALID;
+    return guard3(h, [&] { h->init_equilibrium(); });
+}
+
+int lbm3d_load_cells(lbm3d_handle *h, const float *cells_aos) {
+    if (!h) return LBM_E_INVALID;
+    return guard3(h, [&] { h->load_cells(cells_aos); });
+}
+
+int lbm3d_run_steps(lbm3d_handle *h, int32_t steps) {
+    if (!h) return LBM_E_INVALID;
+    return guard3(h, [&] { h->run_steps(steps); });
+}
+
+int lbm3d_store(lbm3d_handle *h, float *cells_aos, float *av_vels, int32_t n_av) {
+    if (!h) return LBM_E_INVALID;
+    return guard3(h, [&] { h->store(cells_aos, av_vels, n_av); });
+}
+
+int lbm3d_last_run_seconds(lbm3d_handle *h, double *seconds) {
+    if (!h || !seconds) return LBM_E_INVALID;
+    *seconds = h->last_seconds;
+    return LBM_OK;
+}
+
+int64_t lbm3d_total_free_cells(lbm3d_handle *h) { return h ? h->free_cells : -1; }
+
+int lbm3d_local_slabs(lbm3d_handle *h, int32_t *z0, int32_t *nz, int32_t max_slabs, int32_t *n_out) {
+    if (!h) return LBM_E_INVALID;
+    const int n = (int)h->slabs.size();
+    if (n_out) *n_out = n;
+    for (int i = 0; i < n && i < max_slabs; ++i) {
+        if (z0) z0[i] = h->slabs[i].z0;
+        if (nz) nz[i] = h->slabs[i].nzs;
+    }
+    return LBM_OK;
+}
+
+const char *lbm3d_last_error(lbm3d_handle *h) { return h ? h->err.c_str() : g_err3.c_str(); }
+
+void lbm3d_destroy(lbm3d_handle *h) {
+    if (!h) return;
+    try {
+        h->destroy();
+    } catch (...) {
+    }
+    delete h;
+}
+
+}  // extern "C"

@@ -57,6 +57,26 @@ class Params:
         return Params(self.nx, self.ny, int(iters), self.reynolds_dim, self.density, self.accel, self.omega)
 
 
+@dataclass(frozen=True)
+class Params3D:
+    """D3Q19 extension (include/lbm3d_hip.h; no reference counterpart)."""
+    nx: int
+    ny: int
+    nz: int
+    max_iters: int
+    density: float
+    accel: float
+    omega: float
+
+
+def channel_obstacles3d(nx: int, ny: int, nz: int) -> np.ndarray:
+    """Wall planes at y = 0 and y = ny-1 (a Poiseuille channel, periodic in x and z)."""
+    o = np.zeros((nz, ny, nx), np.uint8)
+    o[:, 0, :] = 1
+    o[:, -1, :] = 1
+    return o
+
+
 def read_obstacles(nx: int, ny: int, filename: str) -> "np.ndarray | None":
     """`x y 1` lines -> uint8[ny][nx] (LbmParams.hpp:92-123). None on failure."""
     data = np.zeros((ny, nx), np.uint8)

@@ -35,6 +35,12 @@ EXPORTED = [
     "lbm_total_free_cells", "lbm_local_rects", "lbm_kernel_in_use", "lbm_steps_per_launch",
     "lbm_last_error", "lbm_destroy",
 ]
+# every symbol include/lbm3d_hip.h declares (D3Q19 extension)
+EXPORTED3D = [
+    "lbm3d_create", "lbm3d_init_equilibrium", "lbm3d_load_cells", "lbm3d_run_steps", "lbm3d_store",
+    "lbm3d_last_run_seconds", "lbm3d_total_free_cells", "lbm3d_local_slabs", "lbm3d_last_error", "lbm3d_destroy",
+]
+Q3 = 19
 
 
 class LbmError(RuntimeError):
@@ -72,6 +78,12 @@ class Config(ctypes.Structure):
         ("flags", ctypes.c_int32),
         ("steps_per_launch", ctypes.c_int32),
     ]
+
+
+class Params3D(ctypes.Structure):
+    """lbm3d_params (include/lbm3d_hip.h)."""
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("nz", ctypes.c_int32), ("max_iters", ctypes.c_int32),
+                ("density", ctypes.c_float), ("accel", ctypes.c_float), ("omega", ctypes.c_float)]
 
 
 class Rect(ctypes.Structure):
@@ -116,6 +128,16 @@ def load_library() -> ctypes.CDLL:
         "lbm_steps_per_launch": ([H], i32),
         "lbm_last_error": ([H], ctypes.c_char_p),
         "lbm_destroy": ([H], None),
+        "lbm3d_create": ([ctypes.POINTER(Params3D), u8p, ctypes.POINTER(Config), ctypes.POINTER(H)], ctypes.c_int),
+        "lbm3d_init_equilibrium": ([H], ctypes.c_int),
+        "lbm3d_load_cells": ([H, f32p], ctypes.c_int),
+        "lbm3d_run_steps": ([H, i32], ctypes.c_int),
+        "lbm3d_store": ([H, f32p, f32p, i32], ctypes.c_int),
+        "lbm3d_last_run_seconds": ([H, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+        "lbm3d_total_free_cells": ([H], i64),
+        "lbm3d_local_slabs": ([H, i32p, i32p, i32, i32p], ctypes.c_int),
+        "lbm3d_last_error": ([H], ctypes.c_char_p),
+        "lbm3d_destroy": ([H], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -255,6 +277,89 @@ class Engine:
     def close(self) -> None:
         if self._h:
             self._L.lbm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Engine3D:
+    """One lbm3d_handle: the D3Q19 extension engine (include/lbm3d_hip.h)."""
+
+    def __init__(self, params, obstacles: np.ndarray, *, parts: int = 1, transport: int = TRANSPORT_LOCAL,
+                 rank: int = 0, world: int = 1, devices=None, unique_id: bytes | None = None):
+        self._L = load_library()
+        self.params = Params3D(int(params.nx), int(params.ny), int(params.nz), int(params.max_iters),
+                               float(params.density), float(params.accel), float(params.omega))
+        obst = np.ascontiguousarray(obstacles, dtype=np.uint8)
+        if obst.size != self.params.nx * self.params.ny * self.params.nz:
+            raise ValueError("obstacles must have nz*ny*nx entries")
+        cfg = Config()
+        cfg.parts = int(world if transport == TRANSPORT_RCCL else parts)
+        cfg.transport = transport
+        cfg.rank, cfg.world = int(rank), int(world)
+        if devices:
+            self._devs = (ctypes.c_int32 * len(devices))(*devices)
+            cfg.devices = self._devs
+            cfg.num_devices = len(devices)
+        if unique_id is not None:
+            self._uid = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+            cfg.rccl_unique_id = self._uid
+        self._h = ctypes.c_void_p()
+        rc = self._L.lbm3d_create(ctypes.byref(self.params), obst.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                  ctypes.byref(cfg), ctypes.byref(self._h))
+        if rc != LBM_OK:
+            raise LbmError(rc, self._L.lbm3d_last_error(None).decode())
+
+    def _check(self, rc: int):
+        if rc != LBM_OK:
+            raise LbmError(rc, self._L.lbm3d_last_error(self._h).decode())
+
+    def init_equilibrium(self) -> None:
+        self._check(self._L.lbm3d_init_equilibrium(self._h))
+
+    def load_cells(self, cells: np.ndarray) -> None:
+        c = np.ascontiguousarray(cells, dtype=np.float32)
+        if c.size != self.params.nx * self.params.ny * self.params.nz * Q3:
+            raise ValueError("cells must be AoS float32[nz][ny][nx][19]")
+        self._check(self._L.lbm3d_load_cells(self._h, _f32(c)))
+
+    def run_steps(self, steps: int) -> None:
+        self._check(self._L.lbm3d_run_steps(self._h, int(steps)))
+
+    def store(self, cells: bool = True, n_av: int = 0):
+        out = np.zeros((self.params.nz, self.params.ny, self.params.nx, Q3), np.float32) if cells else None
+        av = np.zeros(max(int(n_av), 1), np.float32)
+        self._check(self._L.lbm3d_store(self._h, _f32(out) if cells else None, _f32(av), int(n_av)))
+        return out, av[:int(n_av)]
+
+    def last_run_seconds(self) -> float:
+        s = ctypes.c_double()
+        self._check(self._L.lbm3d_last_run_seconds(self._h, ctypes.byref(s)))
+        return s.value
+
+    def total_free_cells(self) -> int:
+        return int(self._L.lbm3d_total_free_cells(self._h))
+
+    def local_slabs(self):
+        n = ctypes.c_int32()
+        z0 = (ctypes.c_int32 * 64)()
+        nz = (ctypes.c_int32 * 64)()
+        self._check(self._L.lbm3d_local_slabs(self._h, z0, nz, 64, ctypes.byref(n)))
+        return [(z0[i], nz[i]) for i in range(n.value)]
+
+    def close(self) -> None:
+        if self._h:
+            self._L.lbm3d_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __enter__(self):

@@ -70,10 +70,53 @@ def lib() -> ctypes.CDLL:
         L.oracle_av_velocity.restype = ctypes.c_float
         L.oracle_pipe_run.argtypes = [P, f32p, u8p, ctypes.c_int, f32p]
         L.oracle_pipe_run.restype = ctypes.c_int
+        P3 = ctypes.POINTER(Oracle3DParams)
+        L.oracle3d_init_equilibrium.argtypes = [P3, f32p]
+        L.oracle3d_free_cells.argtypes = [P3, u8p]
+        L.oracle3d_free_cells.restype = ctypes.c_int64
+        L.oracle3d_step.argtypes = [P3, f32p, f32p, u8p]
+        L.oracle3d_step.restype = ctypes.c_float
+        L.oracle3d_run.argtypes = [P3, f32p, u8p, ctypes.c_int, f32p]
+        L.oracle3d_run.restype = ctypes.c_int
         L.oracle_reynolds.argtypes = [P, ctypes.c_float]
         L.oracle_reynolds.restype = ctypes.c_float
         _lib = L
     return _lib
+
+
+class Oracle3DParams(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("nz", ctypes.c_int32), ("max_iters", ctypes.c_int32),
+                ("density", ctypes.c_float), ("accel", ctypes.c_float), ("omega", ctypes.c_float)]
+
+
+def _p3(p) -> Oracle3DParams:
+    return Oracle3DParams(int(p.nx), int(p.ny), int(p.nz), int(p.max_iters), float(p.density), float(p.accel),
+                          float(p.omega))
+
+
+def init_cells3d(params) -> np.ndarray:
+    """D3Q19 equilibrium at rest, AoS float32[nz][ny][nx][19] (oracle/lbm_oracle3d.c)."""
+    cells = np.empty((params.nz, params.ny, params.nx, 19), np.float32)
+    lib().oracle3d_init_equilibrium(ctypes.byref(_p3(params)), _f(cells))
+    return cells
+
+
+def free_cells3d(params, obst: np.ndarray) -> int:
+    return int(lib().oracle3d_free_cells(ctypes.byref(_p3(params)), _u8(np.ascontiguousarray(obst, np.uint8))))
+
+
+def run3d(params, obst: np.ndarray, iters: int, cells: np.ndarray | None = None):
+    """D3Q19 restatement: `iters` steps. Returns (final_cells, av_vels[iters]). Parity unpinned
+    w.r.t. the reference (no 3-D code upstream)."""
+    if cells is None:
+        cells = init_cells3d(params)
+    cells = np.ascontiguousarray(cells, dtype=np.float32).copy()
+    av = np.zeros(max(int(iters), 1), np.float32)
+    rc = lib().oracle3d_run(ctypes.byref(_p3(params)), _f(cells), _u8(np.ascontiguousarray(obst, np.uint8)),
+                            int(iters), _f(av))
+    if rc != 0:
+        raise MemoryError("oracle3d_run allocation failed")
+    return cells, av[:int(iters)]
 
 
 def _p(params) -> OracleParams:

@@ -21,10 +21,22 @@ from lbm_amd import io as lio
 from lbm_amd import native
 
 
-def header_symbols():
-    text = (ROOT / "include" / "lbm_hip.h").read_text()
+def header_symbols(name="lbm_hip.h", prefix="lbm_"):
+    text = (ROOT / "include" / name).read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(lbm_[a-z_0-9]+)\s*\(", text)))
+    return sorted(set(re.findall(rf"\b({prefix}[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_d3q19_symbol():
+    L = native.load_library()
+    syms = header_symbols("lbm3d_hip.h", "lbm3d_")
+    assert len(syms) == 10
+    assert sorted(native.EXPORTED3D) == syms
+    out = subprocess.run(["nm", "-D", "--defined-only", str(native.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    for s in syms:
+        assert hasattr(L, s), s
+        assert re.search(rf"\bT {s}\b", out), s
 
 
 def test_library_exports_every_declared_symbol():

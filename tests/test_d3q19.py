@@ -1,0 +1,173 @@
+"""D3Q19 extension (BASELINE config 5) -- parity UNPINNED
+with respect to the reference, which has no 3-D code.
+
+What pins it instead:
+* CPU: the restatement (oracle/lbm_oracle3d.c) reproduces the analytic
+  Poiseuille profile between bounce-back wall planes, conserves mass, and
+  keeps a z-mirror-symmetric state symmetric;
+* GPU (through the C ABI, include/lbm3d_hip.h): the HIP lattice is BITWISE
+  equal to the restatement -- one slab, z slabs on one GPU (device-copy
+  halos), and the RCCL exchange path (one rank sending its faces to itself).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from lbm_amd import io as lio
+from oracle import oracle
+
+CX = np.array([0, 1, -1, 0, 0, 1, -1, 1, -1, 0, 1, -1, 0, 0, 0, -1, 1, 0, 0])
+CY = np.array([0, 0, 0, 1, -1, 1, -1, -1, 1, 0, 0, 0, 1, -1, 0, 0, 0, -1, 1])
+CZ = np.array([0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1])
+OPP = np.array([0, 2, 1, 4, 3, 6, 5, 8, 7, 14, 15, 16, 17, 18, 9, 10, 11, 12, 13])
+
+
+def test_velocity_set():
+    for k in range(19):
+        assert (CX[OPP[k]], CY[OPP[k]], CZ[OPP[k]]) == (-CX[k], -CY[k], -CZ[k])
+    assert sorted(zip(CX, CY, CZ)) == sorted({(x, y, z) for x in (-1, 0, 1) for y in (-1, 0, 1)
+                                              for z in (-1, 0, 1) if abs(x) + abs(y) + abs(z) <= 2})
+    assert list(np.nonzero(CZ == 1)[0]) == [9, 10, 11, 12, 13]     # one contiguous halo block per face
+    assert list(np.nonzero(CZ == -1)[0]) == [14, 15, 16, 17, 18]
+
+
+def test_oracle3d_equilibrium_moments():
+    p = lio.Params3D(3, 4, 5, 0, 0.7, 0.0, 1.0)
+    c = oracle.init_cells3d(p)
+    np.testing.assert_allclose(c.sum(-1), 0.7, rtol=1e-6)
+    assert np.all((c * CX).sum(-1) == 0) and np.all((c * CY).sum(-1) == 0) and np.all((c * CZ).sum(-1) == 0)
+
+
+def test_oracle3d_poiseuille():
+    """Body force between wall planes y = 0, ny-1 -> steady parabolic u_x(y) with the
+    walls half way between the wall and the first fluid node (bounce-back)."""
+    nx, ny, nz = 4, 18, 4
+    p = lio.Params3D(nx, ny, nz, 0, 1.0, 1e-5, 1.0)
+    cells, _ = oracle.run3d(p, lio.channel_obstacles3d(nx, ny, nz), 6000)
+    ux = (cells * CX).sum(-1) / cells.sum(-1)
+    nu = (1 / p.omega - 0.5) / 3
+    g = p.density * p.accel / 3          # momentum added per step and cell: 2 w1 + 8 w2 = rho a / 3
+    y = np.arange(ny)
+    ana = g / (2 * nu) * (y - 0.5) * (ny - 1.5 - y)
+    prof = ux[:, 1:-1, :]
+    assert np.max(np.abs(prof - ana[None, 1:-1, None])) < 1e-2 * ana.max()
+    assert np.ptp(prof, axis=(0, 2)).max() < 1e-9   # invariant in x and z
+
+
+def test_oracle3d_mass_conservation_and_symmetry():
+    nx, ny, nz = 6, 7, 8
+    p = lio.Params3D(nx, ny, nz, 0, 0.1, 0.0, 1.7)
+    rng = np.random.default_rng(3)
+    obst = lio.channel_obstacles3d(nx, ny, nz)
+    obst[2:6, 3, 2] = 1
+    c0 = (oracle.init_cells3d(p) * (1 + 0.02 * rng.standard_normal((nz, ny, nx, 19)))).astype(np.float32)
+    # z-mirror symmetric start: state(z) = mirror(state(nz-1-z)) with c_z flipped
+    zflip = np.array([k if CZ[k] == 0 else OPP[k] if CX[k] == 0 and CY[k] == 0 else
+                      [j for j in range(19) if (CX[j], CY[j], CZ[j]) == (CX[k], CY[k], -CZ[k])][0]
+                      for k in range(19)])
+    c0 = 0.5 * (c0 + c0[::-1][..., zflip])
+    obst = np.maximum(obst, obst[::-1])
+    m0 = c0.sum(dtype=np.float64)
+    c, _ = oracle.run3d(p, obst, 50, c0)
+    assert c.sum(dtype=np.float64) == pytest.approx(m0, rel=1e-6)
+    np.testing.assert_allclose(c, c[::-1][..., zflip], rtol=1e-4, atol=1e-7)
+
+
+# ------------------------------------------------------------------ GPU ----
+
+def _problem(nx, ny, nz, seed, accel=0.002):
+    p = lio.Params3D(nx, ny, nz, 0, 0.1, accel, 1.7)
+    rng = np.random.default_rng(seed)
+    obst = lio.channel_obstacles3d(nx, ny, nz)
+    obst[rng.random((nz, ny, nx)) < 0.05] = 1
+    c0 = (oracle.init_cells3d(p) * (1 + 0.02 * rng.standard_normal((nz, ny, nx, 19)))).astype(np.float32)
+    return p, obst, c0
+
+
+def _gpu3d(native, p, obst, c0, steps, **kw):
+    with native.Engine3D(p, obst, **kw) as e:
+        e.load_cells(c0)
+        e.run_steps(steps)
+        cells, av = e.store(n_av=steps)
+        assert e.total_free_cells() == int((obst == 0).sum())
+    return cells, av
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nx,ny,nz", [(13, 9, 7), (64, 8, 5), (1, 5, 3), (130, 3, 2)])
+def test_d3q19_bitwise_single_slab(gpu_lib, nx, ny, nz):
+    p, obst, c0 = _problem(nx, ny, nz, nx + ny + nz)
+    ref, ref_av = oracle.run3d(p, obst, 9, c0)
+    cells, av = _gpu3d(gpu_lib, p, obst, c0, 9, devices=[0])
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [2, 3, 4, 7])
+def test_d3q19_slabs_loopback_bitwise(gpu_lib, parts):
+    """z slabs on GPU 0 with device-copy halos (ragged extents), boundary planes on
+    their own stream overlapping the interior."""
+    p, obst, c0 = _problem(20, 11, 15, parts)
+    ref, ref_av = oracle.run3d(p, obst, 12, c0)
+    cells, av = _gpu3d(gpu_lib, p, obst, c0, 12, parts=parts, devices=[0])
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_d3q19_rccl_self_exchange_bitwise(gpu_lib):
+    """World of one over RCCL: the faces go through ncclSend/ncclRecv to itself."""
+    p, obst, c0 = _problem(24, 10, 9, 11)
+    ref, ref_av = oracle.run3d(p, obst, 10, c0)
+    uid = gpu_lib.rccl_unique_id()
+    cells, av = _gpu3d(gpu_lib, p, obst, c0, 10, transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1, devices=[0],
+                       unique_id=uid)
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_d3q19_poiseuille_and_reruns(gpu_lib):
+    """Channel flow to steady state in two runs (state carried over): bitwise equal
+    to the restatement, and the profile is the analytic parabola."""
+    nx, ny, nz = 4, 18, 4
+    p = lio.Params3D(nx, ny, nz, 0, 1.0, 1e-5, 1.0)
+    obst = lio.channel_obstacles3d(nx, ny, nz)
+    ref, _ = oracle.run3d(p, obst, 6000)
+    with gpu_lib.Engine3D(p, obst, devices=[0]) as e:
+        e.init_equilibrium()
+        e.run_steps(2500)
+        e.run_steps(3500)
+        cells, _ = e.store()
+    assert np.array_equal(cells, ref)
+    ux = (cells * CX).sum(-1) / cells.sum(-1)
+    y = np.arange(ny)
+    ana = p.density * p.accel / 3 / (2 * (1 / p.omega - 0.5) / 3) * (y - 0.5) * (ny - 1.5 - y)
+    assert np.max(np.abs(ux[:, 1:-1, :] - ana[None, 1:-1, None])) < 1e-2 * ana.max()
+
+
+@pytest.mark.gpu
+def test_d3q19_256cube_steps_and_mass(gpu_lib):
+    """256^3 on one GPU: 2 steps bitwise vs the restatement, then mass conserved
+    over 50 steps."""
+    n = 256
+    p = lio.Params3D(n, n, n, 0, 0.1, 0.001, 1.85)
+    obst = lio.channel_obstacles3d(n, n, n)
+    c0 = oracle.init_cells3d(p)
+    ref, ref_av = oracle.run3d(p, obst, 2, c0)
+    with gpu_lib.Engine3D(p, obst, devices=[0]) as e:
+        e.init_equilibrium()
+        e.run_steps(2)
+        cells, av = e.store(n_av=2)
+        assert np.array_equal(cells, ref)
+        # the restatement sums 1.6e7 |u| terms sequentially in fp32, which
+        # stagnates once the running sum's ulp nears a term (-7 % here); the GPU
+        # sums in trees.  Tight av_vels checks live on the small grids above.
+        np.testing.assert_allclose(av, ref_av, rtol=0.1)
+        m0 = cells.sum(dtype=np.float64)
+        e.run_steps(50)
+        cells2, av2 = e.store(n_av=50)
+    assert cells2.sum(dtype=np.float64) == pytest.approx(m0, rel=1e-5)
+    assert np.all(np.isfinite(av2)) and av2[-1] > av2[0]

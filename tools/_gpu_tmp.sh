@@ -2,6 +2,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
-  "400|pipe_tests|python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_cli.py -x -v --timeout 200 --timeout-method thread -k 'pipeline'" \
-  "200|prof_pipe|rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pipe -o pipe --output-format csv -- python3 bench.py --kernel pipeline --steps 50 --warmup 2 --no-cpu-baseline --no-aux"
-cat gpurun_out/prof_pipe.log | grep metric
+  "400|d3q19_tests|python -u -m pytest tests/test_d3q19.py -x -q --timeout 200 --timeout-method thread" \
+  "200|bench3d|python tools/bench3d.py --n 512 --steps 50 && python tools/bench3d.py --n 512 --steps 50 --parts 4" \
+  "200|prof3d|rocprofv3 --kernel-trace --stats -d gpurun_out/prof3d -o d3 --output-format csv -- python3 tools/bench3d.py --n 512 --steps 30"
