@@ -778,11 +778,19 @@ struct lbm_handle {
         // (smallest tile height with one tile per CU first, except that 2-row
         // tiles are slower than 4-row ones on every grid measured:
         // profiles/r01/resident/)
-        if (p.nx % 2 == 0 && res_version != 1) order = {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2};
-        if (res_version != 2) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});
+        // v3 (register-resident) only on request: with every wave owning full
+        // rows, the west / east edge populations are finished at the END of the
+        // collision phase and the hop to the neighbours is exposed -- 6.3 us per
+        // step at 1024^2 against 4.8 for v2's boundary-first schedule
+        // (profiles/r01/resident/ab_v2_v3.log, trace_v3.log)
+        if (p.nx % 128 == 0 && res_version == 3) order = {RES3_4, RES3_8, RES3_16, RES3_32, RES3_32x8, RES3_2};
+        if (p.nx % 2 == 0 && (res_version == 0 || res_version == 2))
+            order.insert(order.end(), {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2});
+        if (res_version == 0 || res_version == 1) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});
         res_variant = -1;
         for (int v : order) {
             if (res_th_env > 0 && RES_TH[v] != res_th_env) continue;
+            if (RES_VER[v] == 3 && p.ny % RES_TH[v] != 0) continue;  // v3: exact tilings only
             const int tx = (p.nx + RES_TWV[v] - 1) / RES_TWV[v];
             const int ty = (p.ny + RES_TH[v] - 1) / RES_TH[v];
             int cap = 0;
