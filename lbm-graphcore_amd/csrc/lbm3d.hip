@@ -22,13 +22,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "lbm3d_hip.h"
-#include "lbm_device.hpp"
+#include "lbm_packed.hpp"
 
 namespace lbm {
 
@@ -152,6 +153,161 @@ __global__ __launch_bounds__(B3X * B3Y) void step3d(Step3Args a) {
     }
 }
 
+// One D3Q19 cell: pulled populations s -> outputs o (the order of
+// oracle/lbm_oracle3d.c cell3d); returns |u| (0 for an obstacle).
+__device__ __forceinline__ float cell3d(const float (&s)[Q3], float (&o)[Q3], bool ob, float omega, float omo,
+                                        float w1, float w2) {
+    if (ob) {
+        o[0] = s[0];
+        o[1] = s[2];
+        o[2] = s[1];
+        o[3] = s[4];
+        o[4] = s[3];
+        o[5] = s[6];
+        o[6] = s[5];
+        o[7] = s[8];
+        o[8] = s[7];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            o[9 + i] = s[14 + i];
+            o[14 + i] = s[9 + i];
+        }
+        return 0.f;
+    }
+    const float rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8] + s[9] + s[10] + s[11] + s[12] +
+                      s[13] + s[14] + s[15] + s[16] + s[17] + s[18];
+    const float ux = ((s[1] + s[5] + s[7] + s[10] + s[16]) - (s[2] + s[6] + s[8] + s[11] + s[15])) / rho;
+    const float uy = ((s[3] + s[5] + s[8] + s[12] + s[18]) - (s[4] + s[6] + s[7] + s[13] + s[17])) / rho;
+    const float uz = ((s[9] + s[10] + s[11] + s[12] + s[13]) - (s[14] + s[15] + s[16] + s[17] + s[18])) / rho;
+    const float usq = ux * ux + uy * uy + uz * uz;
+    const float c = 1.00f - usq * 1.50f;
+    const float ld0 = rho / 3.00f * omega;
+    const float ld1 = rho / 18.00f * omega;
+    const float ld2 = rho / 36.00f * omega;
+    const float pxy = ux + uy, mxy = ux - uy, pxz = ux + uz, mxz = -ux + uz, pyz = uy + uz, myz = -uy + uz;
+    const float e[Q3] = {0.f, ux, -ux, uy, -uy, pxy, -pxy, mxy, -mxy, uz, pxz, mxz, pyz, myz,
+                         -uz, -pxz, -mxz, -pyz, -myz};
+    o[0] = s[0] * omo + ld0 * c;
+#pragma unroll
+    for (int k = 1; k < Q3; ++k) {
+        const float ld = (k <= 4 || k == 9 || k == 14) ? ld1 : ld2;
+        o[k] = s[k] * omo + ld * ((4.50f * e[k]) * (2.00f / 3.00f + e[k]) + c);
+    }
+    o[1] = o[1] + w1;
+    o[2] = o[2] - w1;
+    o[5] = o[5] + w2;
+    o[6] = o[6] - w2;
+    o[7] = o[7] + w2;
+    o[8] = o[8] - w2;
+    o[10] = o[10] + w2;
+    o[11] = o[11] - w2;
+    o[15] = o[15] - w2;
+    o[16] = o[16] + w2;
+    return sqrtf(usq);
+}
+
+// Two cells per lane (a column pair, nx even): every load and store is a
+// float2 (512 B per wave instruction instead of 256); the x-shifted pulls
+// take the neighbour column from the adjacent lane by DPP, and the first /
+// last pair of a wave (or of a row, with the periodic wrap) loads it
+// directly.  Each block walks ZB planes, so the per-step |u| partials are
+// ZB times fewer.  Bitwise equal to step3d (same cell3d arithmetic).
+template <int ZB, bool NT>
+__global__ __launch_bounds__(B3X * B3Y) void step3d_pair(Step3Args a, int planes) {
+    __shared__ float lds[B3X * B3Y / 64];
+    const int lane = threadIdx.x;
+    const int xa = blockIdx.x * (2 * B3X) + 2 * lane;
+    const int y = blockIdx.y * B3Y + threadIdx.y;
+    const bool active = xa < a.nx && y < a.ny;
+    float usum = 0.f;
+    const long long PL = a.PL, KS = a.KS;
+    const int px = a.px, nx = a.nx;
+    const int yc = min(y, a.ny - 1);  // inactive rows read a valid row
+    const int ys = yc == 0 ? a.ny - 1 : yc - 1, yn = yc + 1 >= a.ny ? 0 : yc + 1;
+    const long long ry = (long long)yc * px, rs = (long long)ys * px, rn = (long long)yn * px;
+    const int xc = min(xa, nx - 2);  // clamped pair base for inactive lanes
+    const bool first = lane == 0 || xa == 0;
+    const bool last = lane == B3X - 1 || xa + 2 >= nx;
+    const int xl = xa == 0 ? nx - 1 : xa - 1;   // column left of the pair (periodic)
+    const int xr = xa + 2 >= nx ? 0 : xa + 2;   // column right of the pair
+    const int zb0 = blockIdx.z * ZB;
+    for (int zi = 0; zi < ZB; ++zi) {
+        const int zl = zb0 + zi;
+        if (zl >= planes) break;
+        const int z = a.z0 + zl;
+        const float *p0 = a.fin + (long long)z * PL;
+        const float *pm = p0 - PL, *pp = p0 + PL;
+        auto L2 = [&](const float *base, int k, long long row) {
+            return *reinterpret_cast<const f2 *>(base + k * KS + row + xc);
+        };
+        f2 s2[Q3];
+        s2[0] = L2(p0, 0, ry);
+        s2[1] = left2(L2(p0, 1, ry));
+        s2[2] = right2(L2(p0, 2, ry));
+        s2[3] = L2(p0, 3, rs);
+        s2[4] = L2(p0, 4, rn);
+        s2[5] = left2(L2(p0, 5, rs));
+        s2[6] = right2(L2(p0, 6, rn));
+        s2[7] = left2(L2(p0, 7, rn));
+        s2[8] = right2(L2(p0, 8, rs));
+        s2[9] = L2(pm, 9, ry);
+        s2[10] = left2(L2(pm, 10, ry));
+        s2[11] = right2(L2(pm, 11, ry));
+        s2[12] = L2(pm, 12, rs);
+        s2[13] = L2(pm, 13, rn);
+        s2[14] = L2(pp, 14, ry);
+        s2[15] = right2(L2(pp, 15, ry));
+        s2[16] = left2(L2(pp, 16, ry));
+        s2[17] = L2(pp, 17, rn);
+        s2[18] = L2(pp, 18, rs);
+        if (first && active) {  // pulls from x - 1: speeds 1, 5, 7, 10, 16
+            s2[1].x = p0[1 * KS + ry + xl];
+            s2[5].x = p0[5 * KS + rs + xl];
+            s2[7].x = p0[7 * KS + rn + xl];
+            s2[10].x = pm[10 * KS + ry + xl];
+            s2[16].x = pp[16 * KS + ry + xl];
+        }
+        if (last && active) {   // pulls from x + 1: speeds 2, 6, 8, 11, 15
+            s2[2].y = p0[2 * KS + ry + xr];
+            s2[6].y = p0[6 * KS + rn + xr];
+            s2[8].y = p0[8 * KS + rs + xr];
+            s2[11].y = pm[11 * KS + ry + xr];
+            s2[15].y = pp[15 * KS + ry + xr];
+        }
+        if (active) {
+            const uint16_t ob2 = *reinterpret_cast<const uint16_t *>(a.obst + ((long long)zl * a.ny + y) * nx + xa);
+            float sa[Q3], sb[Q3], oa[Q3], obv[Q3];
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) {
+                sa[k] = s2[k].x;
+                sb[k] = s2[k].y;
+            }
+            usum += cell3d(sa, oa, (ob2 & 0xffu) != 0, a.omega, a.omo, a.w1, a.w2);
+            usum += cell3d(sb, obv, (ob2 >> 8) != 0, a.omega, a.omo, a.w1, a.w2);
+            float *d = a.fout + (long long)z * PL + ry + xa;
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) {
+                if (NT)
+                    __builtin_nontemporal_store(f2{oa[k], obv[k]}, reinterpret_cast<f2 *>(d + k * KS));
+                else
+                    *reinterpret_cast<f2 *>(d + k * KS) = f2{oa[k], obv[k]};
+            }
+        }
+    }
+    float v = usum;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    const int t = threadIdx.y * B3X + threadIdx.x;
+    if ((t & 63) == 0) lds[t >> 6] = v;
+    __syncthreads();
+    if (t == 0) {
+        float b = lds[0];
+#pragma unroll
+        for (int i = 1; i < B3X * B3Y / 64; ++i) b += lds[i];
+        a.partials[((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = b;
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void reduce3d(const float *partials, int n, float *av_local, int t) {
     __shared__ float lds[BLOCK / 64];
     const float v = sum_partials_n<BLOCK>(partials, n, lds);
@@ -240,6 +396,11 @@ struct lbm3d_handle {
     int parts = 1, transport = LBM_TRANSPORT_LOCAL, rank = 0, world = 1;
     int px = 0;
     long long KS = 0, PL = 0;
+    bool pair = true;  // column-pair kernel (nx even; LBM3D_PAIR=0 forces the one-cell kernel)
+    // tuned at 512^3 (profiles/r01/d3q19/ab_zb_nt.log): 2 planes per block,
+    // non-temporal stores (the lattice written now is read a whole step later)
+    int zb = 2;        // LBM3D_ZB: planes per block of the pair kernel (1, 2, 4, 8)
+    bool nt = true;    // LBM3D_NT: non-temporal output stores
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
     ncclComm_t comm = nullptr;
@@ -271,6 +432,10 @@ struct lbm3d_handle {
         free_cells = 0;
         for (long long i = 0; i < cells; ++i) free_cells += obstacles[i] ? 0 : 1;
         px = (p.nx + 15) / 16 * 16;  // 64-byte rows
+        const char *pe = getenv("LBM3D_PAIR");
+        pair = p.nx % 2 == 0 && !(pe && *pe && atoi(pe) == 0);
+        if (const char *z = getenv("LBM3D_ZB")) zb = (atoi(z) == 1 || atoi(z) == 4 || atoi(z) == 8) ? atoi(z) : 2;
+        if (const char *n = getenv("LBM3D_NT")) nt = atoi(n) != 0;
         KS = (long long)p.ny * px;
         PL = (long long)Q3 * KS;
         // round-robin z extents (StructuredGridUtils.hpp:161-165 rule, in z)
@@ -330,6 +495,8 @@ struct lbm3d_handle {
     }
 
     int blocks_for(int planes) const {
+        if (pair)
+            return ((p.nx + 2 * B3X - 1) / (2 * B3X)) * ((p.ny + B3Y - 1) / B3Y) * ((std::max(planes, 0) + zb - 1) / zb);
         return ((p.nx + B3X - 1) / B3X) * ((p.ny + B3Y - 1) / B3Y) * std::max(planes, 0);
     }
 
@@ -344,9 +511,10 @@ struct lbm3d_handle {
         const size_t ob = (size_t)s.nzs * p.ny * p.nx;
         H3(hipMalloc(&s.obst, ob + 256));
         H3(hipMemcpy(s.obst, obstacles + (size_t)s.z0 * p.ny * p.nx, ob, hipMemcpyHostToDevice));
-        s.nblk_all = blocks_for(s.nzs);
-        s.nblk_bnd = multi() ? blocks_for(s.nzs >= 2 ? 2 : 1) : 0;
+        // multi: two one-plane boundary launches, then the interior launch
+        s.nblk_bnd = multi() ? (s.nzs >= 2 ? 2 : 1) * blocks_for(1) : 0;
         s.nblk_int = multi() ? blocks_for(s.nzs - 2) : 0;
+        s.nblk_all = multi() ? s.nblk_bnd + s.nblk_int : blocks_for(s.nzs);
         H3(hipMalloc(&s.partials, sizeof(float) * (size_t)(s.nblk_all + 64)));
         H3(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
         H3(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
@@ -451,8 +619,17 @@ struct lbm3d_handle {
         a.w1 = w1();
         a.w2 = w2();
         a.partials = partials;
-        dim3 grid((p.nx + B3X - 1) / B3X, (p.ny + B3Y - 1) / B3Y, planes);
-        hipLaunchKernelGGL(step3d, grid, dim3(B3X, B3Y), 0, st, a);
+        if (pair) {
+            dim3 grid((p.nx + 2 * B3X - 1) / (2 * B3X), (p.ny + B3Y - 1) / B3Y, (planes + zb - 1) / zb);
+            auto k = zb == 1 ? (nt ? step3d_pair<1, true> : step3d_pair<1, false>)
+                   : zb == 2 ? (nt ? step3d_pair<2, true> : step3d_pair<2, false>)
+                   : zb == 8 ? (nt ? step3d_pair<8, true> : step3d_pair<8, false>)
+                             : (nt ? step3d_pair<4, true> : step3d_pair<4, false>);
+            hipLaunchKernelGGL(k, grid, dim3(B3X, B3Y), 0, st, a, planes);
+        } else {
+            dim3 grid((p.nx + B3X - 1) / B3X, (p.ny + B3Y - 1) / B3Y, planes);
+            hipLaunchKernelGGL(step3d, grid, dim3(B3X, B3Y), 0, st, a);
+        }
         H3(hipGetLastError());
     }
 

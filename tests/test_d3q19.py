@@ -95,8 +95,12 @@ def _gpu3d(native, p, obst, c0, steps, **kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nx,ny,nz", [(13, 9, 7), (64, 8, 5), (1, 5, 3), (130, 3, 2)])
-def test_d3q19_bitwise_single_slab(gpu_lib, nx, ny, nz):
+@pytest.mark.parametrize("pair", ["1", "0"])
+@pytest.mark.parametrize("nx,ny,nz", [(13, 9, 7), (64, 8, 5), (1, 5, 3), (130, 3, 2), (2, 6, 3), (256, 5, 9),
+                                      (138, 7, 6)])
+def test_d3q19_bitwise_single_slab(gpu_lib, nx, ny, nz, pair, monkeypatch):
+    """Column-pair kernel (even nx) and one-cell kernel, partial blocks in x, y, z."""
+    monkeypatch.setenv("LBM3D_PAIR", pair)
     p, obst, c0 = _problem(nx, ny, nz, nx + ny + nz)
     ref, ref_av = oracle.run3d(p, obst, 9, c0)
     cells, av = _gpu3d(gpu_lib, p, obst, c0, 9, devices=[0])
