@@ -196,6 +196,7 @@ struct lbm_handle {
     bool resident = false;
     int res_variant = -1;    // ResVariant (LBM_RES_TH picks the tile height)
     int res_th_env = 0;
+    int res_per_cu = 1;      // LBM_RES_PER_CU: tiles per CU the choice may plan for (1 or 2)
     int res_version = 0;     // LBM_RES_V: 1 = scalar 64-column tiles, 2 = packed 128-column tiles, 0 = by grid
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
@@ -251,6 +252,7 @@ struct lbm_handle {
         stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         res_th_env = std::max(0, env_int("LBM_RES_TH", 0));
         res_version = env_int("LBM_RES_V", 0);
+        res_per_cu = std::min(std::max(env_int("LBM_RES_PER_CU", res_per_cu), 1), 2);
         resident_max_cells = std::max(0, env_int("LBM_RES_MAX_CELLS", (int)resident_max_cells));
         if (const char *k = getenv("LBM_KERNEL")) {
             const std::string v(k);
@@ -785,7 +787,7 @@ struct lbm_handle {
         // (profiles/r01/resident/ab_v2_v3.log, trace_v3.log)
         if (p.nx % 128 == 0 && res_version == 3) order = {RES3_4, RES3_8, RES3_16, RES3_32, RES3_32x8, RES3_2};
         if (p.nx % 2 == 0 && (res_version == 0 || res_version == 2))
-            order.insert(order.end(), {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2});
+            order.insert(order.end(), {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2, RES2_16x8});
         if (res_version == 0 || res_version == 1) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});
         res_variant = -1;
         for (int v : order) {
@@ -796,7 +798,7 @@ struct lbm_handle {
             int cap = 0;
             HIP_CHECK(resident_capacity(v, s.dev, cap));
             const long long n = (long long)tx * ty;
-            if (n <= cap && n <= cus) {
+            if (n <= cap && n <= (long long)res_per_cu * cus) {
                 res_variant = v;
                 res_tx = tx;
                 res_ty = ty;

@@ -312,8 +312,8 @@ __global__ __launch_bounds__(64 * NW) void resident_steps(ResidentArgs a) {
 // aligned): the unshifted pulls (N, S) are one ds_read_b64, the shifted ones
 // one ds_read2_b32, every write-back one ds_write_b64.
 // ---------------------------------------------------------------------------
-template <int NW, int TH>
-__global__ __launch_bounds__(64 * NW) void resident_steps2(ResidentArgs a) {
+template <int NW, int TH, int MINW = 1>
+__global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a) {
     constexpr int NT = 64 * NW;
     constexpr int LS = RES2_TW + 4;
     constexpr int PS = (TH + 2) * LS;
@@ -827,9 +827,9 @@ const void *resident_fn() {
     return reinterpret_cast<const void *>(&resident_steps<NW, R>);
 }
 
-template <int NW, int TH>
+template <int NW, int TH, int MINW = 1>
 const void *resident_fn2() {
-    return reinterpret_cast<const void *>(&resident_steps2<NW, TH>);
+    return reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW>);
 }
 
 template <int NW, int R>
@@ -847,6 +847,7 @@ const void *resident_kernel(int variant, int &threads) {
         case RES_4: threads = 256; return resident_fn<4, 1>();
         case RES2_32: threads = 1024; return resident_fn2<16, 32>();
         case RES2_16: threads = 1024; return resident_fn2<16, 16>();
+        case RES2_16x8: threads = 512; return resident_fn2<8, 16, 4>();  // 2 blocks per CU: 4 waves per SIMD
         case RES2_8: threads = 512; return resident_fn2<8, 8>();
         case RES2_4: threads = 256; return resident_fn2<4, 4>();
         case RES2_2: threads = 128; return resident_fn2<2, 2>();

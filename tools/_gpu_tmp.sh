@@ -2,5 +2,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
-  "400|d3q19_tests|python -u -m pytest tests/test_d3q19.py -x -q --timeout 200 --timeout-method thread" \
-  "200|prof3d|rocprofv3 --kernel-trace --stats -d gpurun_out/prof3d -o d3 --output-format csv -- python3 tools/bench3d.py --n 512 --steps 30"
+  "200|res16x8_test|LBM_RES_PER_CU=2 LBM_RES_TH=16 LBM_RES_V=2 python -u -m pytest 'tests/test_gpu_parity.py::test_resident_1024_runs_continue[2]' -x -q --timeout 120 --timeout-method thread" \
+  "200|ab1024|python tools/ab_bench.py --n 1024 --steps 2000 --rounds 3 --variant v2:LBM_KERNEL=resident,LBM_RES_V=2 --variant v2x2:LBM_KERNEL=resident,LBM_RES_V=2,LBM_RES_PER_CU=2,LBM_RES_TH=16 --variant v2x2t:LBM_KERNEL=resident,LBM_RES_V=2,LBM_RES_PER_CU=2,LBM_RES_TH=16,LBM_RES_TRACE=1"
+grep -h "trace\]\|mlups" gpurun_out/ab1024.log
