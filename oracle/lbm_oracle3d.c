@@ -137,3 +137,31 @@ int oracle3d_run(const oracle3d_params *p, float *cells, const uint8_t *obst, in
     free(tmp);
     return 0;
 }
+
+/*
+ * Same step on a z slab of nzs planes with one ghost plane below and above:
+ * `old` is AoS [(nzs+2)][ny][nx][19] (ghost planes at 0 and nzs+1, only the
+ * speeds that cross into the slab need be valid: 9..13 below, 14..18 above),
+ * `out` is [nzs][ny][nx][19]; x and y wrap.  Used by the multi-rank
+ * decomposition test (tests/test_d3q19_gloo.py).
+ */
+float oracle3d_step_slab(const oracle3d_params *p, int nzs, const float *old, float *out, const uint8_t *obst)
+{
+    const int nx = p->nx, ny = p->ny;
+    const float omega = p->omega, omo = 1 - p->omega;
+    const float w1 = p->density * p->accel / 18.f, w2 = p->density * p->accel / 36.f;
+    float tot = 0.00f;
+    for (int z = 0; z < nzs; z++)
+        for (int y = 0; y < ny; y++)
+            for (int x = 0; x < nx; x++) {
+                float s[Q3];
+                for (int k = 0; k < Q3; k++) {
+                    const int xs = (x - CX[k] + nx) % nx, ys = (y - CY[k] + ny) % ny, zs = z + 1 - CZ[k];
+                    s[k] = old[(((size_t)zs * ny + ys) * nx + xs) * Q3 + k];
+                }
+                const size_t idx = ((size_t)z * ny + y) * nx + x;
+                const float u = cell3d(s, out + idx * Q3, obst[idx], omega, omo, w1, w2);
+                if (u >= 0.f) tot += u;
+            }
+    return tot;
+}

@@ -77,6 +77,8 @@ def lib() -> ctypes.CDLL:
         L.oracle3d_step.argtypes = [P3, f32p, f32p, u8p]
         L.oracle3d_step.restype = ctypes.c_float
         L.oracle3d_run.argtypes = [P3, f32p, u8p, ctypes.c_int, f32p]
+        L.oracle3d_step_slab.argtypes = [P3, ctypes.c_int, f32p, f32p, u8p]
+        L.oracle3d_step_slab.restype = ctypes.c_float
         L.oracle3d_run.restype = ctypes.c_int
         L.oracle_reynolds.argtypes = [P, ctypes.c_float]
         L.oracle_reynolds.restype = ctypes.c_float
@@ -117,6 +119,16 @@ def run3d(params, obst: np.ndarray, iters: int, cells: np.ndarray | None = None)
     if rc != 0:
         raise MemoryError("oracle3d_run allocation failed")
     return cells, av[:int(iters)]
+
+
+def step3d_slab(params, ghosted: np.ndarray, obst_slab: np.ndarray):
+    """One D3Q19 step of a z slab given its ghosted input [(nzs+2)][ny][nx][19].
+    Returns (out [nzs][ny][nx][19], tot_u)."""
+    nzs = ghosted.shape[0] - 2
+    out = np.empty((nzs, params.ny, params.nx, 19), np.float32)
+    tot = lib().oracle3d_step_slab(ctypes.byref(_p3(params)), nzs, _f(np.ascontiguousarray(ghosted, np.float32)),
+                                   _f(out), _u8(np.ascontiguousarray(obst_slab, np.uint8)))
+    return out, float(np.float32(tot))
 
 
 def _p(params) -> OracleParams:
