@@ -126,6 +126,25 @@ def cpu_baseline() -> dict | None:
                           f"{secs:.2f} s, 1 thread"}
 
 
+def cpu_baseline_threads() -> dict:
+    """Informational all-cores CPU number ('the build's CPU restatement
+    with OpenMP'): oracle_run_mt on the 1024x1024 reference problem, 60 steps, on
+    OMP_NUM_THREADS threads (16 on the GPU box), lattice bitwise equal to the
+    single-thread restatement."""
+    from oracle import oracle  # checker / baseline only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    gold = ROOT / "tests" / "golden" / "params"
+    p = lio.Params.from_file(str(gold / "input_1024x1024.params")).with_iters(60)
+    obst = lio.read_obstacles(p.nx, p.ny, str(gold / "obstacles_1024x1024.dat"))
+    oracle.run_mt(p, obst, 2, threads)  # warm the thread pool
+    t = time.perf_counter()
+    oracle.run_mt(p, obst, 60, threads)
+    secs = time.perf_counter() - t
+    return {"value": round(1024 * 1024 * 60 / secs / 1e6, 1), "unit": "MLUPS", "cores": threads, "kind": "port",
+            "sample": f"oracle/lbm_oracle.c oracle_run_mt (OpenMP rows), 1024x1024 reference problem, 60 steps, "
+                      f"{secs:.2f} s"}
+
+
 def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
     """BASELINE config 2: the reference 1024x1024 problem, all 20 000 steps, 1 GPU."""
     gold = ROOT / "tests" / "golden" / "params"
@@ -361,6 +380,10 @@ def main() -> int:
             except Exception as exc:
                 out["cpu_baseline"] = None
                 log(f"cpu baseline failed: {exc}")
+            try:
+                out.setdefault("aux", {})["cpu_baseline_threads"] = cpu_baseline_threads()
+            except Exception as exc:
+                log(f"threaded cpu baseline failed: {exc}")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist_on:

@@ -373,3 +373,65 @@ int oracle_pipe_run(const oracle_params *p, float *cells, const uint8_t *obst, i
     free(tmp);
     return 0;
 }
+
+/*
+ * Multi-threaded run for the informational all-cores CPU baseline (bench.py
+ * aux.cpu_baseline_threads): the same per-cell update as oracle_step with the
+ * rows split over `threads` OpenMP threads.  The lattice is bitwise the same;
+ * the per-step |u| sum is added per row and then over rows in row order, so
+ * av_vels can differ from oracle_run in the last bits.
+ */
+int oracle_run_mt(const oracle_params *p, float *cells, const uint8_t *obst, int iters, float *av_vels, int threads)
+{
+    const size_t n = (size_t)p->nx * (size_t)p->ny * Q;
+    float *tmp = (float *)malloc(n * sizeof(float));
+    float *rows = (float *)malloc((size_t)p->ny * sizeof(float));
+    if (!tmp || !rows) {
+        free(tmp);
+        free(rows);
+        return -1;
+    }
+    const float free_cells = (float)oracle_free_cells(p, obst);
+    oracle_accelerate(p, cells, obst);
+    const int nx = p->nx, ny = p->ny;
+    const float w1 = p->density * p->accel / 9.f, w2 = p->density * p->accel / 36.f;
+    const float omega = p->omega, omo = 1 - p->omega;
+    float *a = cells, *b = tmp;
+    for (int t = 0; t < iters; t++) {
+#pragma omp parallel for num_threads(threads) schedule(static)
+        for (int y = 0; y < ny; y++) {
+            const int yn = (y + 1) % ny, ys = (y == 0) ? ny - 1 : y - 1;
+            const float accel_flag = (y == ny - 2) ? 1.00f : 0.00f;
+            float row_u = 0.00f;
+            for (int x = 0; x < nx; x++) {
+                const int xe = (x + 1) % nx, xw = (x == 0) ? nx - 1 : x - 1;
+                float s[Q];
+#define AT(xx, yy, k) a[((size_t)(yy) * nx + (xx)) * Q + (k)]
+                s[0] = AT(x, y, 0);
+                s[1] = AT(xw, y, 1);
+                s[2] = AT(x, ys, 2);
+                s[3] = AT(xe, y, 3);
+                s[4] = AT(x, yn, 4);
+                s[5] = AT(xw, ys, 5);
+                s[6] = AT(xe, ys, 6);
+                s[7] = AT(xe, yn, 7);
+                s[8] = AT(xw, yn, 8);
+#undef AT
+                const size_t idx = (size_t)y * nx + x;
+                const float u = cell_update(s, b + idx * Q, obst[idx], accel_flag, omega, omo, w1, w2);
+                if (u >= 0.f) row_u += u;
+            }
+            rows[y] = row_u;
+        }
+        float tot = 0.00f;
+        for (int y = 0; y < ny; y++) tot += rows[y];
+        if (av_vels) av_vels[t] = tot / free_cells;
+        float *sw = a;
+        a = b;
+        b = sw;
+    }
+    if (a != cells) memcpy(cells, a, n * sizeof(float));
+    free(tmp);
+    free(rows);
+    return 0;
+}

@@ -68,6 +68,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_run.restype = ctypes.c_int
         L.oracle_av_velocity.argtypes = [P, f32p, u8p]
         L.oracle_av_velocity.restype = ctypes.c_float
+        L.oracle_run_mt.argtypes = [P, f32p, u8p, ctypes.c_int, f32p, ctypes.c_int]
+        L.oracle_run_mt.restype = ctypes.c_int
         L.oracle_pipe_run.argtypes = [P, f32p, u8p, ctypes.c_int, f32p]
         L.oracle_pipe_run.restype = ctypes.c_int
         P3 = ctypes.POINTER(Oracle3DParams)
@@ -201,6 +203,20 @@ def run(params, obst: np.ndarray, iters: int | None = None, cells: np.ndarray | 
     if rc != 0:
         raise MemoryError("oracle_run allocation failed")
     return cells, av[:iters]
+
+
+def run_mt(params, obst: np.ndarray, iters: int, threads: int, cells: np.ndarray | None = None):
+    """oracle_run on `threads` OpenMP threads (informational all-cores CPU baseline);
+    the lattice is bitwise equal to run()."""
+    if cells is None:
+        cells = init_cells(params)
+    cells = np.ascontiguousarray(cells, dtype=np.float32).copy()
+    av = np.zeros(max(int(iters), 1), np.float32)
+    rc = lib().oracle_run_mt(ctypes.byref(_p(params)), _f(cells), _u8(np.ascontiguousarray(obst, np.uint8)),
+                             int(iters), _f(av), int(threads))
+    if rc != 0:
+        raise MemoryError("oracle_run_mt allocation failed")
+    return cells, av[:int(iters)]
 
 
 def pipe_run(params, obst: np.ndarray, iters: int | None = None, cells: np.ndarray | None = None):

@@ -72,7 +72,8 @@ def test_compare_lbm_128x256(gpu_lib, tmp_path):
 def test_graph_replay_bitwise(gpu_lib, graph_steps):
     p, obst = load_problem("128x128", iters=301)
     cells0 = lio.init_cells(p)
-    with gpu_lib.Engine(p, obst, graph_steps=graph_steps) as e:
+    # graphs replay the launch-per-step-group kernels (the resident kernel needs none)
+    with gpu_lib.Engine(p, obst, graph_steps=graph_steps, kernel=gpu_lib.KERNEL_STEP2) as e:
         e.load_cells(cells0)
         e.run()
         e.run_steps(17)

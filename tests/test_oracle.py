@@ -197,3 +197,12 @@ def test_pipe_oracle_reference_gate_128():
     ref = lcheck.load_av_vels(GOLD / "check" / "128x128.av_vels.dat.gz")
     d = lcheck.diff_values(ref, av.astype(np.float64))
     assert abs(d["max_diff_pcnt"]) < 1.0
+
+
+def test_oracle_mt_bitwise():
+    """The OpenMP restatement (all-cores CPU baseline) gives the same lattice."""
+    p, obst = load_problem("128x256", iters=40)
+    a, av_a = oracle.run(p, obst, 40)
+    b, av_b = oracle.run_mt(p, obst, 40, 4)
+    assert np.array_equal(a, b)
+    np.testing.assert_allclose(av_b, av_a, rtol=1e-4)  # row-wise partial sums

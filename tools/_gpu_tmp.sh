@@ -2,6 +2,5 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
-  "200|res16x8_test|LBM_RES_PER_CU=2 LBM_RES_TH=16 LBM_RES_V=2 python -u -m pytest 'tests/test_gpu_parity.py::test_resident_1024_runs_continue[2]' -x -q --timeout 120 --timeout-method thread" \
-  "200|ab1024|python tools/ab_bench.py --n 1024 --steps 2000 --rounds 3 --variant v2:LBM_KERNEL=resident,LBM_RES_V=2 --variant v2x2:LBM_KERNEL=resident,LBM_RES_V=2,LBM_RES_PER_CU=2,LBM_RES_TH=16 --variant v2x2t:LBM_KERNEL=resident,LBM_RES_V=2,LBM_RES_PER_CU=2,LBM_RES_TH=16,LBM_RES_TRACE=1"
-grep -h "trace\]\|mlups" gpurun_out/ab1024.log
+  "300|pf_tests|LBM_STREAM_PF=2 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k 'stream or large or open'" \
+  "300|ab_pf|python tools/ab_bench.py --n 8192 --steps 200 --rounds 4 --variant pf1:LBM_STREAM_PF=1 --variant pf2:LBM_STREAM_PF=2 && python tools/ab_bench.py --n 4096 --steps 400 --rounds 3 --variant pf1:LBM_STREAM_PF=1 --variant pf2:LBM_STREAM_PF=2"
