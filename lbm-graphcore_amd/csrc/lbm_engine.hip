@@ -197,6 +197,7 @@ struct lbm_handle {
     int res_variant = -1;    // ResVariant (LBM_RES_TH picks the tile height)
     int res_th_env = 0;
     int res_per_cu = 1;      // LBM_RES_PER_CU: tiles per CU the choice may plan for (1 or 2)
+    int res_early_poll = 0;  // LBM_RES_EARLY: v2 polls the ring after its first work item
     int res_version = 0;     // LBM_RES_V: 1 = scalar 64-column tiles, 2 = packed 128-column tiles, 0 = by grid
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
@@ -253,6 +254,7 @@ struct lbm_handle {
         res_th_env = std::max(0, env_int("LBM_RES_TH", 0));
         res_version = env_int("LBM_RES_V", 0);
         res_per_cu = std::min(std::max(env_int("LBM_RES_PER_CU", res_per_cu), 1), 2);
+        res_early_poll = env_int("LBM_RES_EARLY", res_early_poll) != 0 ? 1 : 0;
         resident_max_cells = std::max(0, env_int("LBM_RES_MAX_CELLS", (int)resident_max_cells));
         if (const char *k = getenv("LBM_KERNEL")) {
             const std::string v(k);
@@ -859,15 +861,57 @@ struct lbm_handle {
             a.partials = res_partials;
             a.status = res_status;
             a.timeout_ticks = res_timeout;
+            a.early_poll = res_early_poll;
             long long *trace = nullptr;
+            unsigned long long *htrace = nullptr;
             const int trace_steps = std::min(steps, 256);
-            if (env_int("LBM_RES_TRACE", 0)) {
+            const int trace_mode = env_int("LBM_RES_TRACE", 0);
+            if (trace_mode) {
                 HIP_CHECK(hipMalloc(&trace, sizeof(long long) * 5 * trace_steps));
                 HIP_CHECK(hipMemsetAsync(trace, 0, sizeof(long long) * 5 * trace_steps, s.s_comp));
                 a.trace = trace;
                 a.trace_steps = trace_steps;
             }
+            if (trace_mode >= 2) {
+                const size_t n = sizeof(unsigned long long) * 2 * trace_steps * ntiles;
+                HIP_CHECK(hipMalloc(&htrace, n));
+                HIP_CHECK(hipMemsetAsync(htrace, 0, n, s.s_comp));
+                a.htrace = htrace;
+            }
             HIP_CHECK(launch_resident(a, res_variant, s.s_comp));
+            if (htrace) {  // per tile and step: wait for the slowest neighbour, then the hop itself
+                std::vector<unsigned long long> hv((size_t)2 * trace_steps * ntiles);
+                HIP_CHECK(hipMemcpyAsync(hv.data(), htrace, hv.size() * 8, hipMemcpyDeviceToHost, s.s_comp));
+                HIP_CHECK(hipStreamSynchronize(s.s_comp));
+                HIP_CHECK(hipFree(htrace));
+                double wait = 0, hop = 0, step = 0, hop_max = 0;
+                long long cnt = 0;
+                for (int t = 2; t + 1 < trace_steps; ++t)
+                    for (int tl = 0; tl < ntiles; ++tl) {
+                        const int tx = tl % res_tx, ty = tl / res_tx;
+                        unsigned long long nbmax = 0;
+                        for (int dy = -1; dy <= 1; ++dy)
+                            for (int dx = -1; dx <= 1; ++dx) {
+                                if (!dx && !dy) continue;
+                                const int nt = ((ty + dy + res_ty) % res_ty) * res_tx + (tx + dx + res_tx) % res_tx;
+                                nbmax = std::max(nbmax, hv[((size_t)t * ntiles + nt) * 2]);
+                            }
+                        const unsigned long long own = hv[((size_t)t * ntiles + tl) * 2];
+                        const unsigned long long ready = hv[((size_t)t * ntiles + tl) * 2 + 1];
+                        wait += (double)nbmax - (double)own;
+                        hop += (double)ready - (double)nbmax;
+                        hop_max = std::max(hop_max, (double)ready - (double)nbmax);
+                        step += (double)hv[((size_t)(t + 1) * ntiles + tl) * 2] - (double)own;
+                        ++cnt;
+                    }
+                int khz = 1;
+                HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.dev));
+                const double us = 1e3 / khz;
+                fprintf(stderr, "[resident hop] %dx%d tile-height %d early_poll %d: per tile-step (us) own collision end -> "
+                        "slowest neighbour's %.3f, -> ring ready %.3f (max %.3f), collision end to next %.3f\n", p.nx,
+                        p.ny, RES_TH[res_variant], res_early_poll, wait / cnt * us, hop / cnt * us, hop_max * us,
+                        step / cnt * us);
+            }
             if (trace) {  // mean phase durations over the traced steps (skipping the first)
                 std::vector<long long> tv((size_t)5 * trace_steps);
                 HIP_CHECK(hipMemcpyAsync(tv.data(), trace, tv.size() * sizeof(long long), hipMemcpyDeviceToHost, s.s_comp));

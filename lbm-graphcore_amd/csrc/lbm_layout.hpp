@@ -204,6 +204,8 @@ struct ResidentArgs {
     long long timeout_ticks;  // wall-clock ticks a poll may wait
     long long *trace;       // LBM_RES_TRACE diagnostics: [step][5] wall-clock stamps of tile 0, wave 0 (or null)
     int trace_steps;
+    unsigned long long *htrace;  // LBM_RES_TRACE=2: [step][tile][2] latest wave's collision end, ring ready
+    int early_poll;         // v2: poll the ring after the first work item instead of after the last
 };
 
 // Halo pack (edge -> dst) after load / accelerate, and unpack (recv -> ghost

@@ -53,15 +53,16 @@ __device__ __forceinline__ void publish(unsigned long long *g, float v, unsigned
     __hip_atomic_store(g, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ float rdlane(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 // Fetch one ring side of step `tag`: positions p = lane + 64 j (j < NPOS,
 // p < len) x the three planes at g[i * RES_GW + p], plus one corner granule
 // cg on lanes that pass one.  Every round issues all outstanding loads back
 // to back (one memory round trip per round, not one per granule) and
 // re-polls only the granules whose tag is not there yet.  v[j * 3 + i] /
 // v[3 * NPOS] receive the values; false on deadline.
-__device__ __forceinline__ float rdlane(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
 
 template <int NPOS>
 __device__ __forceinline__ bool fetch_ring(const unsigned long long *g, int len, const unsigned long long *cg,
@@ -437,12 +438,50 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         }
         __syncthreads();
         if (tr) a.trace[t * 5 + 1] = (long long)wall_clock64();
-        // 2. collide, write back, publish
+        // 2. collide, write back, publish; 3. the neighbours' step-t
+        // populations into the ring (the ring slots are read only by the next
+        // step's pull, so the poll may run while other waves still collide:
+        // with early_poll the polling waves wait right after their first --
+        // boundary -- item, hiding the hop behind the remaining items)
         const unsigned tag = a.tag0 + (unsigned)t + 1u;
         const int slot = t & 1;
         float tot = 0.f;
+        bool ok = true;
+        auto poll_ring = [&]() {
+            const long long deadline = (long long)wall_clock64() + deadline_span;
+            for (int side = wv; side < 4; side += NW) {
+                const int len = side < 2 ? tw : th;
+                const int src_tile = side == 0 ? tys * a.tiles_x + tx
+                                   : side == 1 ? tyn * a.tiles_x + tx
+                                   : side == 2 ? ty * a.tiles_x + txw
+                                               : ty * a.tiles_x + txe;
+                const int d = side == 0 ? DN : side == 1 ? DS : side == 2 ? DE : DW;
+                const bool corner = side < 2 && lane < 2, left = lane == 0;
+                const int cd = side == 0 ? (left ? DNE : DNW) : (left ? DSE : DSW);
+                const unsigned long long *cg =
+                    corner ? gbase(slot, (side == 0 ? tys : tyn) * a.tiles_x + (left ? txw : txe), cd) : nullptr;
+                float v[7];
+                ok = ok && fetch_ring<2>(gbase(slot, src_tile, d), len, cg, tag, deadline, v);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int p = lane + 64 * j;
+                    if (p >= len) continue;
+                    const int lx = side < 2 ? p : (side == 2 ? -1 : tw);
+                    const int ly = side >= 2 ? p : (side == 0 ? -1 : th);
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) L[LJ(PLANES[d][i], ly, lx)] = v[3 * j + i];
+                }
+                if (corner) L[LJ(PLANES[cd][0], side == 0 ? -1 : th, left ? -1 : tw)] = v[6];
+            }
+            if (a.htrace && t < a.trace_steps && wv < 4 && lane == 0)
+                atomicMax(&a.htrace[((long long)t * ntiles + tile) * 2 + 1], (unsigned long long)wall_clock64());
+        };
+        const int poll_it = (a.early_poll && MAXIT >= 2) ? 0 : MAXIT - 1;
 #pragma unroll
         for (int it = 0; it < MAXIT; ++it) {
+            // the poll runs where the wave is converged: never while some of
+            // its lanes still have to publish (a tile can be its own neighbour)
+            if (it > 0 && it - 1 == poll_it) poll_ring();
             if (!((valid >> it) & 1u)) continue;
             const int lx = lxs[it], ly = lys[it];
             const float accf = (gy0 + ly == a.accel_row) ? 1.00f : 0.00f;
@@ -489,37 +528,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
                 publish(g + 2 * RES_GW, o[7].x, tag);
             }
         }
+        if (a.htrace && t < a.trace_steps && lane == 0)
+            atomicMax(&a.htrace[((long long)t * ntiles + tile) * 2], (unsigned long long)wall_clock64());
+        if (poll_it == MAXIT - 1) poll_ring();
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) tot += __shfl_down(tot, off, 64);
         if (lane == 0) wsum[wv] = tot;
         if (tr) a.trace[t * 5 + 2] = (long long)wall_clock64();
-        // 3. neighbours' step-t populations into the ring (sides as v1)
-        bool ok = true;
-        const long long deadline = (long long)wall_clock64() + deadline_span;
-        for (int side = wv; side < 4; side += NW) {
-            const int len = side < 2 ? tw : th;
-            const int src_tile = side == 0 ? tys * a.tiles_x + tx
-                               : side == 1 ? tyn * a.tiles_x + tx
-                               : side == 2 ? ty * a.tiles_x + txw
-                                           : ty * a.tiles_x + txe;
-            const int d = side == 0 ? DN : side == 1 ? DS : side == 2 ? DE : DW;
-            const bool corner = side < 2 && lane < 2, left = lane == 0;
-            const int cd = side == 0 ? (left ? DNE : DNW) : (left ? DSE : DSW);
-            const unsigned long long *cg =
-                corner ? gbase(slot, (side == 0 ? tys : tyn) * a.tiles_x + (left ? txw : txe), cd) : nullptr;
-            float v[7];
-            ok = ok && fetch_ring<2>(gbase(slot, src_tile, d), len, cg, tag, deadline, v);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int p = lane + 64 * j;
-                if (p >= len) continue;
-                const int lx = side < 2 ? p : (side == 2 ? -1 : tw);
-                const int ly = side >= 2 ? p : (side == 0 ? -1 : th);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) L[LJ(PLANES[d][i], ly, lx)] = v[3 * j + i];
-            }
-            if (corner) L[LJ(PLANES[cd][0], side == 0 ? -1 : th, left ? -1 : tw)] = v[6];
-        }
         if (tr) a.trace[t * 5 + 3] = (long long)wall_clock64();
         if (!ok) {
             abort_flag = 1;
