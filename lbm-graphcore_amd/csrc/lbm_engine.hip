@@ -198,7 +198,7 @@ struct lbm_handle {
     int res_th_env = 0;
     int res_per_cu = 1;      // LBM_RES_PER_CU: tiles per CU the choice may plan for (1 or 2)
     int res_early_poll = 0;  // LBM_RES_EARLY: v2 polls the ring after its first work item
-    int res_version = 0;     // LBM_RES_V: 1 = scalar 64-column tiles, 2 = packed 128-column tiles, 0 = by grid
+    int res_version = 0;     // LBM_RES_V: 1 scalar 64-col tiles, 2 packed 128-col, 3 register-resident, 4 AA LDS; 0 = by grid
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
     float *res_partials = nullptr;
@@ -788,6 +788,7 @@ struct lbm_handle {
         // step at 1024^2 against 4.8 for v2's boundary-first schedule
         // (profiles/r01/resident/ab_v2_v3.log, trace_v3.log)
         if (p.nx % 128 == 0 && res_version == 3) order = {RES3_4, RES3_8, RES3_16, RES3_32, RES3_32x8, RES3_2};
+        if (p.nx % 2 == 0 && res_version == 4) order = {RES4_4, RES4_8, RES4_16, RES4_32, RES4_2, RES4_16x8};
         if (p.nx % 2 == 0 && (res_version == 0 || res_version == 2))
             order.insert(order.end(), {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2, RES2_16x8});
         if (res_version == 0 || res_version == 1) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});

@@ -179,12 +179,15 @@ enum ResVariant : int {
     RES_64 = 0, RES_32 = 1, RES_16 = 2, RES_16x4 = 3, RES_8 = 4, RES_4 = 5,           // v1
     RES2_32 = 6, RES2_16 = 7, RES2_8 = 8, RES2_4 = 9, RES2_2 = 10,                    // v2
     RES3_32 = 11, RES3_32x8 = 12, RES3_16 = 13, RES3_8 = 14, RES3_4 = 15, RES3_2 = 16,  // v3
-    RES2_16x8 = 17                                                                      // v2, 8 waves: 2 tiles per CU
+    RES2_16x8 = 17,                                                                     // v2, 8 waves: 2 tiles per CU
+    RES4_32 = 18, RES4_16 = 19, RES4_8 = 20, RES4_4 = 21, RES4_2 = 22,                 // v4: v2 tiles, AA pattern
+    RES4_16x8 = 23                                                                      // v4, 8 waves: 2 tiles per CU
 };
-constexpr int NUM_RES = 18;
-constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 32, 32, 16, 8, 4, 2, 16};
-constexpr int RES_TWV[NUM_RES] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
-constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 2};
+constexpr int NUM_RES = 24;
+constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 32, 32, 16, 8, 4, 2, 16, 32, 16, 8, 4, 2, 16};
+constexpr int RES_TWV[NUM_RES] = {64,  64,  64,  64,  64,  64,  128, 128, 128, 128, 128, 128,
+                                  128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
+constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 2, 4, 4, 4, 4, 4, 4};
 constexpr int RES_GW = 128;  // granule positions per (tile, direction, plane), both versions
 
 struct ResidentArgs {

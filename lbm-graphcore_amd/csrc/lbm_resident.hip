@@ -42,6 +42,8 @@
 // partials[t][tile]; resident_reduce folds the tiles in a fixed order into
 // av_local[t] after the launch.
 
+#include <type_traits>
+
 #include "lbm_packed.hpp"
 
 namespace lbm {
@@ -312,8 +314,26 @@ __global__ __launch_bounds__(64 * NW) void resident_steps(ResidentArgs a) {
 // LDS rows hold 132 floats (ring column at x = -1 and x = tw, pairs 8-byte
 // aligned): the unshifted pulls (N, S) are one ds_read_b64, the shifted ones
 // one ds_read2_b32, every write-back one ds_write_b64.
+//
+// v4 = v2 with AA-pattern LDS addressing (AA = true): the tile keeps ONE copy
+// of populations 1..8 and alternates two representations, so that within a
+// step every LDS slot is read and then written by the same cell and the
+// barrier between pull and write-back disappears (one barrier per step; a
+// wave's LDS reads overlap other waves' collisions):
+//   even step: s_k = F[k][x]            -> o_k into F[opp k][x]       (local)
+//   odd step:  s_k = F[opp k][x - c_k]  -> o_k into F[k][x + c_k]     (pull, push)
+// Slot (y, j) is touched in an odd step only by cell y - c_j, so a tile's
+// ring slots are its own edge cells' targets.  The ring is filled after an
+// even step (neighbours' o_k -> F[opp k][ring]); after an odd step the
+// neighbours' pushed o_k land directly in this tile's edge slots
+// F[k][ring + c_k].  Same granules, same publish sets as v2; the lattice
+// enters as pulled populations and leaves as post-collision ones.
 // ---------------------------------------------------------------------------
-template <int NW, int TH, int MINW = 1>
+__device__ constexpr int res_cx(int k) { return (k == 1 || k == 5 || k == 8) ? 1 : (k == 3 || k == 6 || k == 7) ? -1 : 0; }
+__device__ constexpr int res_cy(int k) { return (k == 2 || k == 5 || k == 6) ? 1 : (k == 4 || k == 7 || k == 8) ? -1 : 0; }
+__device__ constexpr int res_opp(int k) { return k == 0 ? 0 : k <= 4 ? (k + 1) % 4 + 1 : (k - 3) % 4 + 5; }
+
+template <int NW, int TH, int MINW = 1, bool AA = false>
 __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a) {
     constexpr int NT = 64 * NW;
     constexpr int LS = RES2_TW + 4;
@@ -335,6 +355,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
     const long long P = a.plane;
     const int pitch = a.pitch;
 #define LJ(k, ly, lx) (((k) - 1) * PS + ((ly) + 1) * LS + ((lx) + 2))
+    // pair at (ly, lx .. lx + 1) of plane k; al: lx even (one 8-byte access)
+#define LD2(k, ly, lx, al) \
+    ((al) ? *reinterpret_cast<const f2 *>(&L[LJ(k, ly, lx)]) : f2{L[LJ(k, ly, lx)], L[LJ(k, ly, (lx) + 1)]})
+#define ST2(k, ly, lx, al, v)                                    \
+    do {                                                         \
+        if (al) {                                                \
+            *reinterpret_cast<f2 *>(&L[LJ(k, ly, lx)]) = (v);    \
+        } else {                                                 \
+            L[LJ(k, ly, lx)] = (v).x;                            \
+            L[LJ(k, ly, (lx) + 1)] = (v).y;                      \
+        }                                                        \
+    } while (0)
+    auto wrapx = [&](int x) { return x < 0 ? x + a.nx : x >= a.nx ? x - a.nx : x; };
+    auto wrapy = [&](int y) { return y < 0 ? y + a.ny : y >= a.ny ? y - a.ny : y; };
     if (threadIdx.x == 0) abort_flag = 0;
 
     // ---- work items: boundary first ----------------------------------------
@@ -374,9 +408,19 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             const int gx = gx0 + 2 * px, gy = gy0 + ly;
             const float *src = a.fin + (long long)gy * pitch + gx;
             f0[it] = *reinterpret_cast<const f2 *>(src);
+            if constexpr (AA) {  // pulled populations: F[k][x] = f_k(x - c_k)
 #pragma unroll
-            for (int k = 1; k < Q; ++k)
-                *reinterpret_cast<f2 *>(&L[LJ(k, ly, 2 * px)]) = *reinterpret_cast<const f2 *>(src + k * P);
+                for (int k = 1; k < Q; ++k) {
+                    const float *row = a.fin + k * P + (long long)wrapy(gy - res_cy(k)) * pitch;
+                    const f2 v = res_cx(k) == 0 ? *reinterpret_cast<const f2 *>(row + gx)
+                                                : f2{row[wrapx(gx - res_cx(k))], row[wrapx(gx + 1 - res_cx(k))]};
+                    *reinterpret_cast<f2 *>(&L[LJ(k, ly, 2 * px)]) = v;
+                }
+            } else {
+#pragma unroll
+                for (int k = 1; k < Q; ++k)
+                    *reinterpret_cast<f2 *>(&L[LJ(k, ly, 2 * px)]) = *reinterpret_cast<const f2 *>(src + k * P);
+            }
             const uint8_t *ob8 = a.obst + (long long)gy * a.nx + gx;
             o0 = ob8[0] != 0;
             o1 = ob8[1] != 0;
@@ -396,8 +440,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             const int gx = ((gx0 + lx) % a.nx + a.nx) % a.nx;
             const int gy = ((gy0 + ly) % a.ny + a.ny) % a.ny;
             const float *src = a.fin + (long long)gy * pitch + gx;
+            if constexpr (AA) {  // read only when a run has zero steps (write-back of pulled state)
 #pragma unroll
-            for (int k = 1; k < Q; ++k) L[LJ(k, ly, lx)] = src[k * P];
+                for (int k = 1; k < Q; ++k)
+                    L[LJ(k, ly, lx)] = a.fin[k * P + (long long)wrapy(gy - res_cy(k)) * pitch + wrapx(gx - res_cx(k))];
+            } else {
+#pragma unroll
+                for (int k = 1; k < Q; ++k) L[LJ(k, ly, lx)] = src[k * P];
+            }
         }
     }
     __syncthreads();
@@ -407,7 +457,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
     };
     const long long deadline_span = a.timeout_ticks;
     int t = 0;
-    for (; t < a.steps; ++t) {
+    // the step body is instantiated per parity (v4's two addressings are
+    // compile-time, so no per-access selects); returns false on abort
+    auto step = [&](auto odd_c) __attribute__((always_inline)) -> bool {
         const bool tr = a.trace && tile == 0 && threadIdx.x == 0 && t < a.trace_steps;
         if (tr) a.trace[t * 5 + 0] = (long long)wall_clock64();
         if (t > 0 && threadIdx.x == 0) {
@@ -417,6 +469,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             a.partials[(long long)(t - 1) * ntiles + tile] = sw;
         }
         // 1. pull
+        constexpr bool odd = AA && decltype(odd_c)::value;
         f2 s[MAXIT][Q];
 #pragma unroll
         for (int it = 0; it < MAXIT; ++it) {
@@ -427,6 +480,17 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             }
             const int lx = lxs[it], ly = lys[it];
             s[it][0] = f0[it];
+            if constexpr (AA) {  // all items' loads back to back; no barrier (each slot is this cell's)
+                if (odd) {
+#pragma unroll
+                    for (int k = 1; k < Q; ++k)
+                        s[it][k] = LD2(res_opp(k), ly - res_cy(k), lx - res_cx(k), res_cx(k) == 0);
+                } else {
+#pragma unroll
+                    for (int k = 1; k < Q; ++k) s[it][k] = LD2(k, ly, lx, true);
+                }
+                continue;
+            }
             s[it][1] = f2{L[LJ(1, ly, lx - 1)], L[LJ(1, ly, lx)]};
             s[it][2] = *reinterpret_cast<const f2 *>(&L[LJ(2, ly - 1, lx)]);
             s[it][3] = f2{L[LJ(3, ly, lx + 1)], L[LJ(3, ly, lx + 2)]};
@@ -436,7 +500,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             s[it][7] = f2{L[LJ(7, ly + 1, lx + 1)], L[LJ(7, ly + 1, lx + 2)]};
             s[it][8] = f2{L[LJ(8, ly + 1, lx - 1)], L[LJ(8, ly + 1, lx)]};
         }
-        __syncthreads();
+        if constexpr (!AA) __syncthreads();
         if (tr) a.trace[t * 5 + 1] = (long long)wall_clock64();
         // 2. collide, write back, publish; 3. the neighbours' step-t
         // populations into the ring (the ring slots are read only by the next
@@ -447,6 +511,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         const int slot = t & 1;
         float tot = 0.f;
         bool ok = true;
+        // neighbour's o_k for ring cell (ly, lx): v2 and after an even v4 step
+        // into the ring slot (plane opp k for v4), after an odd v4 step pushed
+        // on into this tile's edge cell (ly, lx) + c_k (dropped when that is
+        // outside the tile: a diagonal tile receives it as a corner granule)
+        auto ring_put = [&](int k, int ly, int lx, float v) {
+            if (!AA) {
+                L[LJ(k, ly, lx)] = v;
+            } else if (!odd) {
+                L[LJ(res_opp(k), ly, lx)] = v;
+            } else {
+                const int ex = lx + res_cx(k), ey = ly + res_cy(k);
+                if (ex >= 0 && ex < tw && ey >= 0 && ey < th) L[LJ(k, ey, ex)] = v;
+            }
+        };
         auto poll_ring = [&]() {
             const long long deadline = (long long)wall_clock64() + deadline_span;
             for (int side = wv; side < 4; side += NW) {
@@ -469,9 +547,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
                     const int lx = side < 2 ? p : (side == 2 ? -1 : tw);
                     const int ly = side >= 2 ? p : (side == 0 ? -1 : th);
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) L[LJ(PLANES[d][i], ly, lx)] = v[3 * j + i];
+                    for (int i = 0; i < 3; ++i) ring_put(PLANES[d][i], ly, lx, v[3 * j + i]);
                 }
-                if (corner) L[LJ(PLANES[cd][0], side == 0 ? -1 : th, left ? -1 : tw)] = v[6];
+                if (corner) ring_put(PLANES[cd][0], side == 0 ? -1 : th, left ? -1 : tw, v[6]);
             }
             if (a.htrace && t < a.trace_steps && wv < 4 && lane == 0)
                 atomicMax(&a.htrace[((long long)t * ntiles + tile) * 2 + 1], (unsigned long long)wall_clock64());
@@ -490,8 +568,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
                                   a.omo, a.w1, a.w2);
             tot += u.x + u.y;
             f0[it] = o[0];
+            if (!AA) {
 #pragma unroll
-            for (int k = 1; k < Q; ++k) *reinterpret_cast<f2 *>(&L[LJ(k, ly, lx)]) = o[k];
+                for (int k = 1; k < Q; ++k) ST2(k, ly, lx, true, o[k]);
+            } else if (odd) {
+#pragma unroll
+                for (int k = 1; k < Q; ++k) ST2(k, ly + res_cy(k), lx + res_cx(k), res_cx(k) == 0, o[k]);
+            } else {
+#pragma unroll
+                for (int k = 1; k < Q; ++k) ST2(res_opp(k), ly, lx, true, o[k]);
+            }
             const bool west = lx == 0, east = lx + 2 == tw;
             if (ly == th - 1) {  // leaving north: 2, 5, 6
                 unsigned long long *g = gbase(slot, tile, DN) + lx;
@@ -542,7 +628,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         }
         __syncthreads();
         if (tr) a.trace[t * 5 + 4] = (long long)wall_clock64();
-        if (abort_flag) break;
+        return !abort_flag;
+    };
+    for (; t < a.steps; ++t) {
+        const bool go = (AA && (t & 1)) ? step(std::true_type{}) : step(std::false_type{});
+        if (!go) break;
     }
     if (t == a.steps && a.steps > 0 && threadIdx.x == 0) {
         float sw = wsum[0];
@@ -557,8 +647,19 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         float *dst = a.fout + (long long)(gy0 + ly) * pitch + gx0 + lx;
         *reinterpret_cast<f2 *>(dst) = f0[it];
 #pragma unroll
-        for (int k = 1; k < Q; ++k) *reinterpret_cast<f2 *>(dst + k * P) = *reinterpret_cast<const f2 *>(&L[LJ(k, ly, lx)]);
+        for (int k = 1; k < Q; ++k) {
+            f2 v;
+            if (!AA)  // v4 after an odd step count: o_k in F[opp k][x]; after an even one: in F[k][x + c_k]
+                v = LD2(k, ly, lx, true);
+            else if (a.steps & 1)
+                v = LD2(res_opp(k), ly, lx, true);
+            else
+                v = LD2(k, ly + res_cy(k), lx + res_cx(k), res_cx(k) == 0);
+            *reinterpret_cast<f2 *>(dst + k * P) = v;
+        }
     }
+#undef ST2
+#undef LD2
 #undef LJ
 }
 
@@ -842,9 +943,9 @@ const void *resident_fn() {
     return reinterpret_cast<const void *>(&resident_steps<NW, R>);
 }
 
-template <int NW, int TH, int MINW = 1>
+template <int NW, int TH, int MINW = 1, bool AA = false>
 const void *resident_fn2() {
-    return reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW>);
+    return reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW, AA>);
 }
 
 template <int NW, int R>
@@ -866,6 +967,12 @@ const void *resident_kernel(int variant, int &threads) {
         case RES2_8: threads = 512; return resident_fn2<8, 8>();
         case RES2_4: threads = 256; return resident_fn2<4, 4>();
         case RES2_2: threads = 128; return resident_fn2<2, 2>();
+        case RES4_32: threads = 1024; return resident_fn2<16, 32, 1, true>();
+        case RES4_16: threads = 1024; return resident_fn2<16, 16, 1, true>();
+        case RES4_8: threads = 512; return resident_fn2<8, 8, 1, true>();
+        case RES4_4: threads = 256; return resident_fn2<4, 4, 1, true>();
+        case RES4_2: threads = 128; return resident_fn2<2, 2, 1, true>();
+        case RES4_16x8: threads = 512; return resident_fn2<8, 16, 4, true>();
         case RES3_32: threads = 1024; return resident_fn3<16, 2>();
         case RES3_32x8: threads = 512; return resident_fn3<8, 4>();
         case RES3_16: threads = 512; return resident_fn3<8, 2>();

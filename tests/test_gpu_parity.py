@@ -359,9 +359,9 @@ def test_open_periodic_random_bitwise(gpu_lib, mode, version, monkeypatch):
 # ------------------------------------------------- resident kernel ----
 
 # (version, tile height): v1 scalar 64-column tiles, v2 packed 128-column tiles
-# v3 register-resident, exact 128 x TH tilings only
+# v3 register-resident, exact 128 x TH tilings only; v4 = v2 tiles, AA-pattern LDS
 RES_VARIANTS = [(1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 2), (2, 4), (2, 8), (2, 16), (2, 32),
-                (3, 2), (3, 4), (3, 8), (3, 16), (3, 32)]
+                (3, 2), (3, 4), (3, 8), (3, 16), (3, 32), (4, 2), (4, 4), (4, 8), (4, 16), (4, 32)]
 
 
 @pytest.mark.parametrize("ver,th", RES_VARIANTS)
@@ -370,7 +370,7 @@ RES_VARIANTS = [(1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 2), (2, 4), (2, 8
 def test_resident_tiles_bitwise(gpu_lib, ver, th, nx, ny, steps, monkeypatch):
     """Every resident tile height on exact and ragged tilings (partial last tiles in
     x and y, one-row and one-column grids): lattice bitwise == oracle."""
-    if ver == 2 and nx % 2:
+    if ver in (2, 4) and nx % 2:
         pytest.skip("the packed resident kernel needs an even width")
     if ver == 3 and (nx % 128 or ny % th):
         pytest.skip("the register-resident kernel needs an exact 128 x TH tiling")
@@ -391,7 +391,7 @@ def test_resident_tiles_bitwise(gpu_lib, ver, th, nx, ny, steps, monkeypatch):
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
-@pytest.mark.parametrize("ver", [1, 2, 3])
+@pytest.mark.parametrize("ver", [1, 2, 3, 4])
 def test_resident_1024_runs_continue(gpu_lib, ver, monkeypatch):
     """1024^2 (BASELINE config 2 grid, 256 co-resident 64x64 tiles): three runs of
     different lengths continue one state (granule tags keep counting across runs),
