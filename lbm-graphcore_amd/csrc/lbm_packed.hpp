@@ -5,7 +5,7 @@
 // Bitwise parity with the one-step kernels and the CPU oracle: every
 // expression is evaluated in the order of LastChance.cpp:226-262 with one
 // rounding per operation (packed ops round each lane like their scalar
-// forms; no contraction).  The three kinds of correctly rounded operations
+// forms; no contraction).  The two kinds of correctly rounded operations
 // use shorter exact sequences than the compiler's general expansions:
 //   * x / 9 and x / 36: q = x*y, r = fma(-d, q, x), q' = fma(r, y, q) with
 //     y = RN(1/d) -- exhaustively checked equal to RN(x/d) over 41 binades
@@ -16,8 +16,7 @@
 //     exponent limits, 0, inf or NaN (densities are ~0.1 and momenta
 //     either 0 or far above 2^-100 in any physical state); the reciprocal
 //     refinement is shared by u_x and u_y;
-//   * sqrt(u^2): v_sqrt_f32 plus the LLVM one-ulp correction steps, without
-//     the 2^32 pre-scaling used only below 2^-96 (0 is still exact).
+// |u| = sqrt(u^2) feeds only av_vels and uses v_sqrt_f32 (sqrt_av below).
 #pragma once
 
 #include "lbm_device.hpp"
@@ -62,16 +61,12 @@ __device__ __forceinline__ void div_pair(f2 nx, f2 ny, f2 d, f2 &qx, f2 &qy) {
     qy = fma2(fma2(nd, p, ny), r, p);
 }
 
-// correctly rounded sqrt for 0 and normal x (see header)
-__device__ __forceinline__ float sqrt_cr(float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sd = __int_as_float(__float_as_int(s) - 1);
-    const float su = __int_as_float(__float_as_int(s) + 1);
-    const float rd = __builtin_fmaf(-sd, s, x);
-    const float ru = __builtin_fmaf(-su, s, x);
-    const float t = (rd <= 0.f) ? sd : s;
-    return (ru > 0.f) ? su : t;
-}
+// |u| for av_vels only (never fed back into the lattice): v_sqrt_f32, within
+// 1 ulp of the correctly rounded sqrtf.  The av_vels sum already differs
+// from the reference's by summation order; this costs < 1e-7 relative per
+// term and saves the 16-instruction correction per cell pair
+// (profiles/r01/final/ab_sqrt.log: +1 % at 8192^2, +5 % resident 1024^2).
+__device__ __forceinline__ float sqrt_av(float x) { return __builtin_amdgcn_sqrtf(x); }
 
 // One cell pair: pulled populations s -> post-collision o; returns |u| per cell (0 for obstacles).
 // any_obst (wave-uniform): some lane of the wave has an obstacle cell in this
@@ -112,7 +107,7 @@ __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bo
         o[7] = f7;
         o[6] = f6;
         o[8] = f8;
-        return f2{sqrt_cr(usq.x), sqrt_cr(usq.y)};
+        return f2{sqrt_av(usq.x), sqrt_av(usq.y)};
     }
     // obstacle cells rebound: out_k = s_opp(k)
     o[0] = f2{oa ? s[0].x : c0.x, ob ? s[0].y : c0.y};
@@ -124,7 +119,7 @@ __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bo
     o[7] = f2{oa ? s[5].x : f7.x, ob ? s[5].y : f7.y};
     o[6] = f2{oa ? s[8].x : f6.x, ob ? s[8].y : f6.y};
     o[8] = f2{oa ? s[6].x : f8.x, ob ? s[6].y : f8.y};
-    return f2{oa ? 0.f : sqrt_cr(usq.x), ob ? 0.f : sqrt_cr(usq.y)};
+    return f2{oa ? 0.f : sqrt_av(usq.x), ob ? 0.f : sqrt_av(usq.y)};
 }
 
 }  // namespace lbm
