@@ -3,11 +3,11 @@ cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 ALT=lbm-graphcore_amd/build/alt/liblbm_hip.so
 bash tools/gpu_steps.sh \
-  "200|cr8192a|python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant cr:" \
-  "200|fast8192a|env LBM_HIP_LIB=$ALT python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant fast:" \
-  "200|cr8192b|python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant cr:" \
-  "200|fast8192b|env LBM_HIP_LIB=$ALT python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant fast:" \
-  "200|cr1024|python tools/ab_bench.py --n 1024 --steps 2000 --rounds 3 --variant cr:" \
-  "200|fast1024|env LBM_HIP_LIB=$ALT python tools/ab_bench.py --n 1024 --steps 2000 --rounds 3 --variant fast:" \
-  "300|fast_tests|env LBM_HIP_LIB=$ALT python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread"
-grep -h "mlups\|passed\|failed" gpurun_out/cr8192a.log gpurun_out/fast8192a.log gpurun_out/cr8192b.log gpurun_out/fast8192b.log gpurun_out/cr1024.log gpurun_out/fast1024.log gpurun_out/fast_tests.log
+  "300|stream_tests|python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_cli.py -x -q --timeout 120 --timeout-method thread -k 'stream or auto or 8192 or exchange or decomp'" \
+  "200|new8192a|python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant buf:" \
+  "200|old8192a|env LBM_HIP_LIB=$ALT python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant old:" \
+  "200|new8192b|python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant buf:" \
+  "200|old8192b|env LBM_HIP_LIB=$ALT python tools/ab_bench.py --n 8192 --steps 200 --rounds 3 --variant old:" \
+  "200|new4096|python tools/ab_bench.py --n 4096 --steps 400 --rounds 3 --variant buf:" \
+  "200|old4096|env LBM_HIP_LIB=$ALT python tools/ab_bench.py --n 4096 --steps 400 --rounds 3 --variant old:"
+grep -h "mlups\|passed\|failed" gpurun_out/stream_tests.log gpurun_out/new8192a.log gpurun_out/old8192a.log gpurun_out/new8192b.log gpurun_out/old8192b.log gpurun_out/new4096.log gpurun_out/old4096.log
