@@ -265,7 +265,6 @@ struct lbm_handle {
         }
         const char *l = getenv("LBM_LAYOUT");
         if (l && *l) row_interleaved = std::string(l) != "planar";
-        if (!row_interleaved) stream_v = 1;  // the packed kernel's buffer offsets assume the rows-interleaved layout
     }
 
     // ---- halo destinations --------------------------------------------

@@ -127,8 +127,8 @@ __global__ __launch_bounds__(BLOCK) void step_vec4(StepArgs a) {
             if (active) {
                 st4(w0 + 1 * P, make_float4(o1[0], o1[1], o1[2], o1[3]));
                 st4(w0 + 3 * P, make_float4(o3[0], o3[1], o3[2], o3[3]));
-                if (east) a.dst[DE].p[0][y * a.dst[DE].ps] = o1[3];
-                if (west) a.dst[DW].p[0][y * a.dst[DW].ps] = o3[0];
+                if (east) a.dst[DE].p[0][(long long)y * a.dst[DE].ps] = o1[3];
+                if (west) a.dst[DW].p[0][(long long)y * a.dst[DW].ps] = o3[0];
             }
         }
         // N / S pair
@@ -155,8 +155,8 @@ __global__ __launch_bounds__(BLOCK) void step_vec4(StepArgs a) {
             if (active) {
                 st4(w0 + 5 * P, k5);
                 st4(w0 + 7 * P, k7);
-                if (east) a.dst[DE].p[1][y * a.dst[DE].ps] = o5[3];
-                if (west) a.dst[DW].p[2][y * a.dst[DW].ps] = o7[0];
+                if (east) a.dst[DE].p[1][(long long)y * a.dst[DE].ps] = o5[3];
+                if (west) a.dst[DW].p[2][(long long)y * a.dst[DW].ps] = o7[0];
                 if (north) {
                     st4(a.dst[DN].p[1] + x0, k5);
                     if (east) a.dst[DNE].p[0][0] = o5[3];
@@ -177,8 +177,8 @@ __global__ __launch_bounds__(BLOCK) void step_vec4(StepArgs a) {
             if (active) {
                 st4(w0 + 6 * P, k6);
                 st4(w0 + 8 * P, k8);
-                if (east) a.dst[DE].p[2][y * a.dst[DE].ps] = o8[3];
-                if (west) a.dst[DW].p[1][y * a.dst[DW].ps] = o6[0];
+                if (east) a.dst[DE].p[2][(long long)y * a.dst[DE].ps] = o8[3];
+                if (west) a.dst[DW].p[1][(long long)y * a.dst[DW].ps] = o6[0];
                 if (north) {
                     st4(a.dst[DN].p[2] + x0, k6);
                     if (west) a.dst[DNW].p[0][0] = o6[0];
@@ -236,15 +236,15 @@ __global__ __launch_bounds__(BLOCK) void step_scalar(StepArgs a) {
         const bool north = (y == a.h - 1), south = (y == 0);
         if (east) {
             const EdgeDst &d = a.dst[DE];
-            d.p[0][y * d.ps] = o[1];
-            d.p[1][y * d.ps] = o[5];
-            d.p[2][y * d.ps] = o[8];
+            d.p[0][(long long)y * d.ps] = o[1];
+            d.p[1][(long long)y * d.ps] = o[5];
+            d.p[2][(long long)y * d.ps] = o[8];
         }
         if (west) {
             const EdgeDst &d = a.dst[DW];
-            d.p[0][y * d.ps] = o[3];
-            d.p[1][y * d.ps] = o[6];
-            d.p[2][y * d.ps] = o[7];
+            d.p[0][(long long)y * d.ps] = o[3];
+            d.p[1][(long long)y * d.ps] = o[6];
+            d.p[2][(long long)y * d.ps] = o[7];
         }
         if (north) {
             const EdgeDst &d = a.dst[DN];

@@ -74,31 +74,9 @@ __global__ __launch_bounds__(64, MINW) void stream_steps2c(StreamArgs a) {
         const int xca = min(xa, (a.xmax - 1) & ~1);
         const long long P = a.plane;
         const int pitch = a.pitch;
+        const float *src = a.fin + xca;
+        const uint8_t *obp = a.obst_g + (xca + a.og);
         const int jlast = yo1 + S - 1;
-        // Buffer resources based at the segment's first row and the strip's
-        // first column: a lane's column offset is the only VGPR address (fixed
-        // for the whole walk), rows and planes go into the scalar soffset
-        // (SALU), replacing nine 64-bit VALU address computations per row and
-        // level.  Offsets stay far below 2^31 (rows-interleaved layout: a plane
-        // row is one 9*rf-float row; the engine uses v1 for the planar layout).
-        const int j0 = yo0 - S;
-        const __amdgpu_buffer_rsrc_t rin =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(a.fin + (long long)j0 * pitch + base), (short)0, -1, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rout =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(a.fout + (long long)yo0 * pitch + base), (short)0, -1, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rob = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(a.obst_g + (long long)(j0 + a.og) * a.ogp + base + a.og), (short)0, -1, 0x00020000);
-        const int vin = (xca - base) * 4, vobst = xca - base, vout = 2 * lane * 4;
-        const int P4 = (int)P * 4, pitch4 = pitch * 4;
-        auto load_row = [&](int jj, f2 (&dst)[Q], unsigned &o0, unsigned &o1) __attribute__((always_inline)) {
-            const int so = (jj - j0) * pitch4;
-#pragma unroll
-            for (int k = 0; k < Q; ++k)
-                dst[k] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rin, vin, so + k * P4, 0));
-            const int sob = (jj - j0) * a.ogp;
-            o0 = __builtin_amdgcn_raw_buffer_load_b8(rob, vobst, sob, 0);
-            o1 = __builtin_amdgcn_raw_buffer_load_b8(rob, vobst + 1, sob, 0);
-        };
 
         f2 c0[S], c1[S], c3[S], a2[S], a5[S], a6[S], b2[S], b5[S], b6[S];
 #pragma unroll
@@ -106,15 +84,25 @@ __global__ __launch_bounds__(64, MINW) void stream_steps2c(StreamArgs a) {
             c0[b] = c1[b] = c3[b] = a2[b] = a5[b] = a6[b] = b2[b] = b5[b] = b6[b] = mk2(0.f);
         unsigned oba = 0, obb = 0;
 
-        int j = j0;
+        int j = yo0 - S;
         f2 v[Q];
         unsigned voa, vob;
-        load_row(j, v, voa, vob);
+        {
+            const float *c = src + (long long)j * pitch;
+#pragma unroll
+            for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const f2 *>(c + k * P);
+            const uint8_t *oc = obp + (long long)(j + a.og) * a.ogp;
+            voa = oc[0];
+            vob = oc[1];
+        }
         for (; j <= jlast; ++j) {
             const int jn = min(j + 1, jlast);
             f2 nv[Q];
-            unsigned nvoa, nvob;
-            load_row(jn, nv, nvoa, nvob);
+            const float *cn = src + (long long)jn * pitch;
+#pragma unroll
+            for (int k = 0; k < Q; ++k) nv[k] = *reinterpret_cast<const f2 *>(cn + k * P);
+            const uint8_t *ocn = obp + (long long)(jn + a.og) * a.ogp;
+            const unsigned nvoa = ocn[0], nvob = ocn[1];
 
             oba = (oba << 1) | (voa != 0 ? 1u : 0u);
             obb = (obb << 1) | (vob != 0 ? 1u : 0u);
@@ -144,22 +132,16 @@ __global__ __launch_bounds__(64, MINW) void stream_steps2c(StreamArgs a) {
                 if (rowlive) tot[b] += f2{owna ? u.x : 0.f, ownb ? u.y : 0.f};
                 if (L == S) {
                     if (rowlive && (owna || ownb)) {
-                        const int so = (y - yo0) * pitch4;
+                        float *w0 = a.fout + (long long)y * pitch + xa;
                         if (owna && ownb) {
 #pragma unroll
-                            for (int k = 0; k < Q; ++k)
-                                __builtin_amdgcn_raw_buffer_store_b64(
-                                    __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o[k]), rout, vout,
-                                    so + k * P4, 0);
+                            for (int k = 0; k < Q; ++k) *reinterpret_cast<f2 *>(w0 + k * P) = o[k];
                         } else if (owna) {
 #pragma unroll
-                            for (int k = 0; k < Q; ++k)
-                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[k].x), rout, vout, so + k * P4, 0);
+                            for (int k = 0; k < Q; ++k) w0[k * P] = o[k].x;
                         } else {
 #pragma unroll
-                            for (int k = 0; k < Q; ++k)
-                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[k].y), rout, vout + 4, so + k * P4,
-                                                                      0);
+                            for (int k = 0; k < Q; ++k) w0[k * P + 1] = o[k].y;
                         }
                         if (xa < S || xb >= a.w - S || y < S || y >= a.h - S) {
                             float oa_[Q], ob_[Q];

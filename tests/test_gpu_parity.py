@@ -317,6 +317,31 @@ def test_stream_segments_bitwise(gpu_lib, version, S, hs, monkeypatch):
             np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
+def test_16384_lattice_64bit_indexing(gpu_lib):
+    """BASELINE config 4's 16384^2 sub-domain holds 2.4e9 floats per lattice (over
+    2^31): every index into it must be 64-bit.  (The one-step kernels' ghost-edge
+    stores once formed y * pitch in 32 bits and faulted there -- reached by the
+    remainder of a step count that is not a multiple of the stream kernel's 4.)
+    6 steps = one 4-step stream launch + two one-step launches, against six
+    one-step (vec4) launches: bitwise equal and finite."""
+    n = 16384
+    p = lio.Params(n, n, 6, 10, 0.1, 0.005, 1.85)
+    obst = np.zeros((n, n), np.uint8)
+    obst[0, :] = obst[-1, :] = 1
+    obst[:, n // 3] = 1
+    runs = {}
+    for name, kw in (("auto", {}), ("vec4", mode_kw(gpu_lib, "vec4"))):
+        with gpu_lib.Engine(p, obst, **kw) as e:
+            e.init_equilibrium()
+            e.run_steps(6, accelerate_first=True)
+            runs[name] = (e.kernel_in_use(), *e.store(n_av=6))
+    assert runs["auto"][0] == "stream" and runs["vec4"][0] == "vec4"
+    a, b = runs["auto"][1], runs["vec4"][1]
+    assert np.isfinite(a[:: 97, :: 89]).all()
+    assert np.array_equal(a, b)
+    np.testing.assert_allclose(runs["auto"][2], runs["vec4"][2], rtol=1e-5)
+
+
 def test_stream_size_limits(gpu_lib):
     """STREAM needs S x S sub-domains (2S across a decomposed dimension); AUTO falls back."""
     p = lio.Params(12, 3, 4, 10, 0.1, 0.005, 1.85)
