@@ -175,3 +175,24 @@ def test_d3q19_256cube_steps_and_mass(gpu_lib):
         cells2, av2 = e.store(n_av=50)
     assert cells2.sum(dtype=np.float64) == pytest.approx(m0, rel=1e-5)
     assert np.all(np.isfinite(av2)) and av2[-1] > av2[0]
+
+
+@pytest.mark.gpu
+def test_d3q19_512cube_64bit_indexing(gpu_lib, monkeypatch):
+    """BASELINE config 5's 512^3 on one GPU: 2.55e9 floats per lattice (over 2^31),
+    so every index into it must be 64-bit.  3 steps of the column-pair kernel and
+    of the one-cell kernel (independent indexing code): bitwise equal, finite."""
+    n = 512
+    p = lio.Params3D(n, n, n, 0, 0.1, 0.001, 1.85)
+    obst = lio.channel_obstacles3d(n, n, n)
+    out = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("LBM3D_PAIR", pair)
+        with gpu_lib.Engine3D(p, obst, devices=[0]) as e:
+            e.init_equilibrium()
+            e.run_steps(3)
+            out[pair] = e.store(n_av=3)
+    (a, av_a), (b, av_b) = out["1"], out["0"]
+    assert np.isfinite(a[::31, ::29, ::37]).all()
+    assert np.array_equal(a, b)
+    np.testing.assert_allclose(av_a, av_b, rtol=1e-5)
