@@ -6,8 +6,9 @@
 // decomposition with halos over RCCL (or device copies), boundary planes on a
 // high-priority stream so the exchange overlaps the interior.
 //
-// Layout per slab of nzs planes: f[z + 1][k][y][px] for -1 <= z <= nzs (one
-// ghost plane below and above); speeds ordered so that the five that cross
+// Layout per slab of nzs planes: f[z + 2][k][y][px] for -2 <= z <= nzs + 1 (two
+// ghost planes below and above: the one-step kernels read the inner ones, the
+// two-step kernel both); speeds ordered so that the five that cross
 // the top face (c_z = +1: 9..13) and the five that cross the bottom face
 // (c_z = -1: 14..18) are each ONE contiguous block of a plane -- the halo
 // message of a face is a single contiguous range of the lattice, sent and
@@ -308,6 +309,161 @@ __global__ __launch_bounds__(B3X * B3Y) void step3d_pair(Step3Args a, int planes
     }
 }
 
+// ---------------------------------------------------------------------------
+// Two time steps per pass over the lattice (one slab, z periodic): 2.5-D
+// temporal blocking.  A block of 64 columns (one wave, one column per lane) x
+// T3H rows (one wave per row) walks a segment of z planes; as input plane j
+// arrives (step t, 19 coalesced loads per lane), level 1 computes plane j-1 at
+// t+1 and level 2 computes plane j-2 at t+2 from level 1's planes, so the
+// lattice crosses HBM once per two steps.  Owned outputs: the inner 60 x
+// (T3H - 4) cells (a two-cell ring in x and y is recomputed).
+// Pulls, per level, for the centre plane z (input plane z+1 just arrived):
+//   own row, x +- 1 by DPP:   speeds 0,1,2 of plane z, 9,10,11 of plane z-1
+//                             (registers kept from earlier iterations),
+//                             14,15,16 of plane z+1;
+//   rows y +- 1 through LDS:  3..8 of plane z (ring of 2 plane slots),
+//                             12,13 of plane z-1 (ring of 3), 17,18 of z+1.
+// Two barriers per iteration (one per level) order every slot's writes and
+// reads (each slot is rewritten only after the barrier that follows its last
+// read).  Algorithmic traffic per cell update: (19 loads x 768/480 + 19
+// stores) x 4 B / 2 = 99 B instead of 152.  Same cell3d arithmetic: bitwise
+// equal to the one-step kernels.
+// ---------------------------------------------------------------------------
+constexpr int T3W = 64, T3H = 12;
+constexpr int T3OX = T3W - 4, T3OY = T3H - 4;
+constexpr int T3C = T3W * T3H;               // cells per plane slot
+constexpr int T3LDS = (2 + 2 * 6 + 3 * 2) * T3C;  // floats per level: M, Z[2][6], P[3][2]
+
+struct Two3Args {
+    const float *fin;   // origin of the lattice read (ghost planes -2, -1, nz, nz + 1 filled)
+    float *fout;
+    const uint8_t *obst;  // [nz][ny][nx]
+    long long PL, KS;
+    int px, nx, ny, nz, seg;
+    float omega, omo, w1, w2;
+    float *partials;      // [2][nblocks]: |u| of step t+1, then t+2
+    int nblocks;
+};
+
+// One level for centre plane jz - 1, input plane jz (in).  Must be reached by
+// every thread of the block (it holds a barrier).
+__device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3], float *lds, int jz, float (&r0)[3],
+                                        float (&r9a)[3], float (&r9b)[3], int lane, int wy, bool ob,
+                                        const Two3Args &a) {
+    float *M = lds, *Z = lds + 2 * T3C, *P = lds + 14 * T3C;
+    const int c = wy * T3W + lane;
+    const int zw = jz & 1, pw = ((jz % 3) + 3) % 3;  // slots of plane jz
+    M[c] = in[17];
+    M[T3C + c] = in[18];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) Z[(zw * 6 + i) * T3C + c] = in[3 + i];
+    P[(pw * 2) * T3C + c] = in[12];
+    P[(pw * 2 + 1) * T3C + c] = in[13];
+    __syncthreads();
+    const int wm = max(wy - 1, 0) * T3W, wp = min(wy + 1, T3H - 1) * T3W;
+    const int lm = max(lane - 1, 0), lp = min(lane + 1, T3W - 1);
+    const float *z = Z + ((jz - 1) & 1) * 6 * T3C;          // plane jz - 1
+    const float *p = P + ((((jz - 2) % 3) + 3) % 3) * 2 * T3C;  // plane jz - 2
+    float s[Q3];
+    s[0] = r0[0];
+    s[1] = dpp_from_left(r0[1]);
+    s[2] = dpp_from_right(r0[2]);
+    s[3] = z[0 * T3C + wm + lane];
+    s[4] = z[1 * T3C + wp + lane];
+    s[5] = z[2 * T3C + wm + lm];
+    s[6] = z[3 * T3C + wp + lp];
+    s[7] = z[4 * T3C + wp + lm];
+    s[8] = z[5 * T3C + wm + lp];
+    s[9] = r9b[0];
+    s[10] = dpp_from_left(r9b[1]);
+    s[11] = dpp_from_right(r9b[2]);
+    s[12] = p[0 * T3C + wm + lane];
+    s[13] = p[1 * T3C + wp + lane];
+    s[14] = in[14];
+    s[15] = dpp_from_right(in[15]);
+    s[16] = dpp_from_left(in[16]);
+    s[17] = M[wp + lane];
+    s[18] = M[T3C + wm + lane];
+    const float u = cell3d(s, out, ob, a.omega, a.omo, a.w1, a.w2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        r9b[i] = r9a[i];
+        r9a[i] = in[9 + i];
+        r0[i] = in[i];
+    }
+    return u;
+}
+
+__global__ __launch_bounds__(T3W * T3H) void step3d_two(Two3Args a) {
+    __shared__ float lds1[T3LDS], lds2[T3LDS];
+    __shared__ float red[2][T3H];
+    const int lane = threadIdx.x, wy = threadIdx.y;
+    const int ox = blockIdx.x * T3OX, oy = blockIdx.y * T3OY;
+    const int x = (((ox - 2 + lane) % a.nx) + a.nx) % a.nx;
+    const int y = (((oy - 2 + wy) % a.ny) + a.ny) % a.ny;
+    const bool own = lane >= 2 && lane < T3W - 2 && wy >= 2 && wy < T3H - 2 && ox + lane - 2 < a.nx &&
+                     oy + wy - 2 < a.ny;
+    const int zs = blockIdx.z * a.seg, ze = min(zs + a.seg, a.nz);
+    const long long row = (long long)y * a.px + x;
+    float r0a[3] = {0.f, 0.f, 0.f}, r9aa[3] = {0.f, 0.f, 0.f}, r9ba[3] = {0.f, 0.f, 0.f};
+    float r0b[3] = {0.f, 0.f, 0.f}, r9ab[3] = {0.f, 0.f, 0.f}, r9bb[3] = {0.f, 0.f, 0.f};
+    float u1 = 0.f, u2 = 0.f;
+    auto obz = [&](int zz) {
+        zz = ((zz % a.nz) + a.nz) % a.nz;
+        return a.obst[((long long)zz * a.ny + y) * a.nx + x] != 0;
+    };
+    // input planes are prefetched one iteration ahead (their loads stay in
+    // flight across the two barriers of the current iteration)
+    float in[Q3];
+    bool ob1 = obz(zs - 3), ob2 = obz(zs - 4);
+    {
+        const float *pl = a.fin + (long long)(zs - 2) * a.PL + row;
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) in[k] = pl[k * a.KS];
+    }
+    for (int j = zs - 2; j <= ze + 1; ++j) {
+        float nin[Q3];
+        const float *pn = a.fin + (long long)min(j + 1, ze + 1) * a.PL + row;
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) nin[k] = pn[k * a.KS];
+        ob2 = ob1;
+        ob1 = obz(j - 1);
+        float o1[Q3], o2[Q3];
+        const float v1 = level3(in, o1, lds1, j, r0a, r9aa, r9ba, lane, wy, ob1, a);
+        if (own && j - 1 >= zs && j - 1 < ze) u1 += v1;
+        const float v2 = level3(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, lane, wy, ob2, a);
+        if (own && j - 2 >= zs && j - 2 < ze) {
+            u2 += v2;
+            float *d = a.fout + (long long)(j - 2) * a.PL + row;
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) __builtin_nontemporal_store(o2[k], d + k * a.KS);
+        }
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) in[k] = nin[k];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        u1 += __shfl_down(u1, off, 64);
+        u2 += __shfl_down(u2, off, 64);
+    }
+    if (lane == 0) {
+        red[0][wy] = u1;
+        red[1][wy] = u2;
+    }
+    __syncthreads();
+    if (lane == 0 && wy == 0) {
+        float b1 = red[0][0], b2 = red[1][0];
+#pragma unroll
+        for (int i = 1; i < T3H; ++i) {
+            b1 += red[0][i];
+            b2 += red[1][i];
+        }
+        const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        a.partials[blk] = b1;
+        a.partials[a.nblocks + blk] = b2;
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void reduce3d(const float *partials, int n, float *av_local, int t) {
     __shared__ float lds[BLOCK / 64];
     const float v = sum_partials_n<BLOCK>(partials, n, lds);
@@ -382,6 +538,8 @@ struct Slab {
     uint8_t *obst = nullptr;
     float *partials = nullptr;
     int nblk_all = 0, nblk_bnd = 0, nblk_int = 0;
+    float *partials2 = nullptr;  // two-step kernel: [2][nblk_two]
+    int nblk_two = 0;
     float *av_local = nullptr;
     int av_cap = 0;
     int cur = 0;
@@ -401,6 +559,8 @@ struct lbm3d_handle {
     // non-temporal stores (the lattice written now is read a whole step later)
     int zb = 2;        // LBM3D_ZB: planes per block of the pair kernel (1, 2, 4, 8)
     bool nt = true;    // LBM3D_NT: non-temporal output stores
+    bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two) on a single slab
+    int seg = 64;      // LBM3D_SEG: z planes per block of the two-step kernel (32-128 equal within noise at 512^3)
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
     ncclComm_t comm = nullptr;
@@ -436,6 +596,8 @@ struct lbm3d_handle {
         pair = p.nx % 2 == 0 && !(pe && *pe && atoi(pe) == 0);
         if (const char *z = getenv("LBM3D_ZB")) zb = (atoi(z) == 1 || atoi(z) == 4 || atoi(z) == 8) ? atoi(z) : 2;
         if (const char *n = getenv("LBM3D_NT")) nt = atoi(n) != 0;
+        if (const char *t = getenv("LBM3D_TWO")) two = atoi(t) != 0;
+        if (const char *g = getenv("LBM3D_SEG")) seg = std::max(1, atoi(g));
         KS = (long long)p.ny * px;
         PL = (long long)Q3 * KS;
         // round-robin z extents (StructuredGridUtils.hpp:161-165 rule, in z)
@@ -502,11 +664,12 @@ struct lbm3d_handle {
 
     void alloc(Slab &s, const uint8_t *obstacles) {
         H3(hipSetDevice(s.dev));
-        const size_t floats = (size_t)(s.nzs + 2) * PL;
+        // two ghost planes below and above (the two-step kernel reads both)
+        const size_t floats = (size_t)(s.nzs + 4) * PL;
         for (int k = 0; k < 2; ++k) {
             H3(hipMalloc(&s.f[k], floats * sizeof(float)));
             H3(hipMemset(s.f[k], 0, floats * sizeof(float)));
-            s.o[k] = s.f[k] + PL;
+            s.o[k] = s.f[k] + 2 * PL;
         }
         const size_t ob = (size_t)s.nzs * p.ny * p.nx;
         H3(hipMalloc(&s.obst, ob + 256));
@@ -516,12 +679,58 @@ struct lbm3d_handle {
         s.nblk_int = multi() ? blocks_for(s.nzs - 2) : 0;
         s.nblk_all = multi() ? s.nblk_bnd + s.nblk_int : blocks_for(s.nzs);
         H3(hipMalloc(&s.partials, sizeof(float) * (size_t)(s.nblk_all + 64)));
+        if (!multi()) {
+            const dim3 g = two_grid(s);
+            s.nblk_two = (int)(g.x * g.y * g.z);
+            H3(hipMalloc(&s.partials2, sizeof(float) * (2 * (size_t)s.nblk_two + 64)));
+        }
         H3(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
         H3(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
         int lo = 0, hi = 0;
         H3(hipDeviceGetStreamPriorityRange(&lo, &hi));
         H3(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, hi));
         for (hipEvent_t *e : {&s.ev_b, &s.ev_i, &s.ev_x, &s.ev_end}) H3(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+
+    dim3 two_grid(const Slab &s) const {
+        return dim3((p.nx + T3OX - 1) / T3OX, (p.ny + T3OY - 1) / T3OY, (s.nzs + seg - 1) / seg);
+    }
+
+    // two-step pass: ghost planes -2, -1, nz, nz + 1 of the current lattice
+    // (periodic images, all 19 speeds), then step3d_two, then both steps' |u|
+    void step_two(int t) {
+        Slab &s = slabs[0];
+        const size_t bytes = sizeof(float) * (size_t)PL;
+        float *o = s.o[s.cur];
+        for (int g : {-2, -1, s.nzs, s.nzs + 1}) {
+            const int src = ((g % s.nzs) + s.nzs) % s.nzs;
+            H3(hipMemcpyAsync(o + (long long)g * PL, o + (long long)src * PL, bytes, hipMemcpyDeviceToDevice, s.s_comp));
+        }
+        Two3Args a{};
+        a.fin = o;
+        a.fout = s.o[1 - s.cur];
+        a.obst = s.obst;
+        a.PL = PL;
+        a.KS = KS;
+        a.px = px;
+        a.nx = p.nx;
+        a.ny = p.ny;
+        a.nz = s.nzs;
+        a.seg = seg;
+        a.omega = p.omega;
+        a.omo = 1 - p.omega;
+        a.w1 = w1();
+        a.w2 = w2();
+        a.partials = s.partials2;
+        a.nblocks = s.nblk_two;
+        hipLaunchKernelGGL(step3d_two, two_grid(s), dim3(T3W, T3H), 0, s.s_comp, a);
+        H3(hipGetLastError());
+        hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials2, s.nblk_two, s.av_local, t);
+        hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials2 + s.nblk_two, s.nblk_two,
+                           s.av_local, t + 1);
+        H3(hipGetLastError());
+        s.cur ^= 1;
+        exchange(s.cur, false);  // faces for a one-step launch that may follow
     }
 
     void ensure_av(int n) {
@@ -705,7 +914,10 @@ struct lbm3d_handle {
             H3(hipEventRecord(s.ev_i, s.s_comp));
             H3(hipEventRecord(s.ev_x, s.s_comp));
         }
-        for (int t = 0; t < steps; ++t) step_once(t);
+        int t = 0;
+        if (!multi() && two)
+            for (; t + 2 <= steps; t += 2) step_two(t);
+        for (; t < steps; ++t) step_once(t);
         for (auto &s : slabs) {
             H3(hipSetDevice(s.dev));
             H3(hipStreamWaitEvent(s.s_comp, s.ev_x, 0));
@@ -727,7 +939,7 @@ struct lbm3d_handle {
         for (auto &s : slabs) {
             H3(hipSetDevice(s.dev));
             s.cur = 0;
-            const long long planes = s.nzs + 2;
+            const long long planes = s.nzs + 4;
             hipLaunchKernelGGL(init3d, dim3((unsigned)((planes * KS + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s.s_comp,
                                s.f[0], planes, KS, PL, c0, c1, c2);
             H3(hipGetLastError());
@@ -815,6 +1027,7 @@ struct lbm3d_handle {
                 if (s.f[k]) (void)hipFree(s.f[k]);
             if (s.obst) (void)hipFree(s.obst);
             if (s.partials) (void)hipFree(s.partials);
+            if (s.partials2) (void)hipFree(s.partials2);
             if (s.av_local) (void)hipFree(s.av_local);
             for (hipStream_t st : {s.s_comp, s.s_bnd, s.s_comm})
                 if (st) (void)hipStreamDestroy(st);

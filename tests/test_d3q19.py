@@ -95,12 +95,17 @@ def _gpu3d(native, p, obst, c0, steps, **kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pair", ["1", "0"])
+@pytest.mark.parametrize("pair,two,seg", [("1", "0", "32"), ("0", "0", "32"), ("1", "1", "32"), ("1", "1", "2"),
+                                          ("0", "1", "1")])
 @pytest.mark.parametrize("nx,ny,nz", [(13, 9, 7), (64, 8, 5), (1, 5, 3), (130, 3, 2), (2, 6, 3), (256, 5, 9),
-                                      (138, 7, 6)])
-def test_d3q19_bitwise_single_slab(gpu_lib, nx, ny, nz, pair, monkeypatch):
-    """Column-pair kernel (even nx) and one-cell kernel, partial blocks in x, y, z."""
+                                      (138, 7, 6), (61, 17, 1), (125, 10, 4)])
+def test_d3q19_bitwise_single_slab(gpu_lib, nx, ny, nz, pair, two, seg, monkeypatch):
+    """Column-pair kernel (even nx) and one-cell kernel, and the two-steps-per-pass
+    kernel (z segments of 32, 2 and 1 planes; 9 steps = four two-step passes + one
+    one-step launch), partial blocks in x, y, z, wrapped tiles (nx < 60)."""
     monkeypatch.setenv("LBM3D_PAIR", pair)
+    monkeypatch.setenv("LBM3D_TWO", two)
+    monkeypatch.setenv("LBM3D_SEG", seg)
     p, obst, c0 = _problem(nx, ny, nz, nx + ny + nz)
     ref, ref_av = oracle.run3d(p, obst, 9, c0)
     cells, av = _gpu3d(gpu_lib, p, obst, c0, 9, devices=[0])
@@ -180,14 +185,16 @@ def test_d3q19_256cube_steps_and_mass(gpu_lib):
 @pytest.mark.gpu
 def test_d3q19_512cube_64bit_indexing(gpu_lib, monkeypatch):
     """BASELINE config 5's 512^3 on one GPU: 2.55e9 floats per lattice (over 2^31),
-    so every index into it must be 64-bit.  3 steps of the column-pair kernel and
-    of the one-cell kernel (independent indexing code): bitwise equal, finite."""
+    so every index into it must be 64-bit.  3 steps as one two-step pass plus one
+    pair-kernel step, and as three one-cell steps (independent indexing code):
+    bitwise equal, finite."""
     n = 512
     p = lio.Params3D(n, n, n, 0, 0.1, 0.001, 1.85)
     obst = lio.channel_obstacles3d(n, n, n)
     out = {}
-    for pair in ("1", "0"):
+    for pair, two in (("1", "1"), ("0", "0")):  # two-step passes + pair kernel; one-cell kernel
         monkeypatch.setenv("LBM3D_PAIR", pair)
+        monkeypatch.setenv("LBM3D_TWO", two)
         with gpu_lib.Engine3D(p, obst, devices=[0]) as e:
             e.init_equilibrium()
             e.run_steps(3)
