@@ -1,7 +1,7 @@
 /* check_fastdiv.c -- CPU evidence for the exact short sequences used by the
  * two-column stream kernel (lbm-graphcore_amd/csrc/lbm_stream2.hip).
  *
- * 1. x / d for d = 9, 36: q = RN(x*y), r = fma(-d, q, x), q' = fma(r, y, q),
+ * 1. x / d for d = 9, 36 (D2Q9) and 3, 18 (D3Q19): q = RN(x*y), r = fma(-d, q, x), q' = fma(r, y, q),
  *    y = RN(1/d).  Checked against IEEE x / d for EVERY float x in 41
  *    binades [2^-20, 2^21) -- the check depends only on the significand while
  *    no result is subnormal, so this covers every normal x of interest.
@@ -41,8 +41,8 @@ static float div_seq(float n, float d, float r0) {
 int main(int argc, char **argv) {
     long pairs = argc > 1 ? atol(argv[1]) : 20000000L;
     long bad = 0, total = 0;
-    const float ds[2] = {9.0f, 36.0f};
-    for (int di = 0; di < 2; ++di) {
+    const float ds[4] = {9.0f, 36.0f, 3.0f, 18.0f};  /* D2Q9 weights; D3Q19 adds 1/3, 1/18 */
+    for (int di = 0; di < 4; ++di) {
         volatile float one = 1.0f, d = ds[di];
         const float y = one / d;
         for (int e = -20; e <= 20; ++e)
