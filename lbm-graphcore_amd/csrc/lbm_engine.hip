@@ -45,6 +45,7 @@ hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hi
 hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t s);
 hipError_t launch_stream(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
 hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s);
+hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
@@ -565,8 +566,28 @@ struct lbm_handle {
         int hs = stream_hs;
         if (hs <= 0) {
             const long long strips = (std::max(x1 - x0, 1) + ow_of(x0) - 1) / ow_of(x0);
+            const long long rows = std::max(y1 - y0, 1);
             const long long target = 8192;
-            hs = (int)std::max<long long>(4LL * S, (std::max(y1 - y0, 1) * strips + target - 1) / target);
+            hs = (int)std::max<long long>(4LL * S, (rows * strips + target - 1) / target);
+            // whole rounds of the device's concurrently resident waves: 8211
+            // waves at 2048 per round ran a fifth round of 19 waves (209 GLUPS
+            // at 8192^2); 8142 waves (four rounds) 217-227, 16215 (eight) 222
+            // (profiles/r01/stream/ab_hs_rounds.log).  Eight rounds where the
+            // segments stay at least 4S rows high, fewer otherwise.
+            int per_cu = 0, cus = 0;
+            if (stream_v == 2 && stream2c_blocks_per_cu(S, stream_waves, per_cu) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev) == hipSuccess &&
+                per_cu > 0 && cus > 0) {
+                const long long cap = (long long)per_cu * cus;
+                const long long nseg_max = std::max<long long>(1, rows / (4LL * S));
+                const long long k_max = std::max<long long>(1, nseg_max * strips / cap);
+                const long long k = std::min<long long>(8, k_max);
+                const long long nseg = std::min(nseg_max, std::max<long long>(1, k * cap / strips));
+                hs = (int)((rows + nseg - 1) / nseg);
+            }
+            if (getenv("LBM_STREAM_DEBUG"))
+                fprintf(stderr, "[stream split] %dx%d: strips %lld rows %lld waves/CU %d CUs %d -> hs %d\n", s.w, s.h,
+                        strips, rows, per_cu, cus, hs);
         }
         auto mk = [&](int rx, int ry, int rw, int rh, int rhs) {
             const int ow = ow_of(rx);

@@ -184,6 +184,16 @@ static void launch_s2c(const StreamArgs &a, int blocks, bool reduce, hipStream_t
         hipLaunchKernelGGL((stream_steps2c<S, false, MINW>), dim3(blocks), dim3(64), 0, s, a);
 }
 
+// Resident 64-thread blocks (waves) per CU of the instantiation a launch with
+// these parameters uses (the engine sizes segments to whole rounds of them).
+hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n) {
+    const bool w3 = waves >= 3;
+    const void *fn = steps == 2   ? (const void *)&stream_steps2c<2, false, 2>
+                     : steps == 3 ? (w3 ? (const void *)&stream_steps2c<3, false, 3> : (const void *)&stream_steps2c<3, false, 2>)
+                                  : (w3 ? (const void *)&stream_steps2c<4, false, 3> : (const void *)&stream_steps2c<4, false, 2>);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, 0);
+}
+
 // waves = minimum waves per SIMD the register allocation targets (2, or 3:
 // fewer registers, some spilled)
 hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s) {

@@ -1,12 +1,6 @@
 #!/bin/bash
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_d3q19.py -x -q --timeout 240 --timeout-method thread -m gpu > gpurun_out/d3_tests.log 2>&1 || { tail -30 gpurun_out/d3_tests.log; exit 1; }
-: > gpurun_out/d3_ab2.log
-for r in 1 2; do
-  for cfg in "0 64" "1 64" "1 128"; do
-    set -- $cfg
-    echo "two=$1 seg=$2 round=$r $(env LBM3D_TWO=$1 LBM3D_SEG=$2 timeout -k 10 120 python tools/bench3d.py --n 512 --steps 40 | tail -n 1)" >> gpurun_out/d3_ab2.log || exit 1
-  done
-done
-tail -1 gpurun_out/d3_tests.log; cat gpurun_out/d3_ab2.log
+bash tools/gpu_steps.sh \
+  "500|hs|python tools/ab_bench.py --n 8192 --steps 500 --rounds 5 --variant auto: --variant h35:LBM_STREAM_HS=35 --variant h69:LBM_STREAM_HS=69 --variant h70:LBM_STREAM_HS=70"
+grep -h mlups gpurun_out/hs.log
