@@ -2,5 +2,10 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
-  "500|hs|python tools/ab_bench.py --n 8192 --steps 500 --rounds 5 --variant auto: --variant h35:LBM_STREAM_HS=35 --variant h69:LBM_STREAM_HS=69 --variant h70:LBM_STREAM_HS=70"
-grep -h mlups gpurun_out/hs.log
+  "900|pytest_gpu|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+  "300|smoke|python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "400|bench|python bench.py" \
+  "300|prof_trace|rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o bench --output-format csv -- python3 bench.py --steps 400 --no-cpu-baseline --no-aux" \
+  "120|pmc_fetch|timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1" \
+  "120|pmc_write|timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1"
+grep -h "passed\|failed" gpurun_out/pytest_gpu.log; tail -2 gpurun_out/smoke.log; tail -1 gpurun_out/bench.log
