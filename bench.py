@@ -11,9 +11,13 @@ Workload (config.workload): BASELINE config 3, 8192x8192 fp32 cells per GPU
 with deterministic synthetic obstacles (walls on the four borders plus one
 full interior column at x = nx/3, mimicking obstacles_1024x1024.dat), rho 0.1,
 accel 0.005, omega 1.85, equilibrium start.  For N > 1 the per-GPU tile is
-fixed (weak scaling): the global grid is (8192*R) x (8192*C) with R x C =
-1x2, 2x2, 2x4 from the reference's partitionForIpus rule, one process per
-GPU, halos over RCCL.  Rank 0 at N=1 also runs BASELINE config 2 (the
+fixed (weak scaling): the tiles are stacked in y, global grid 8192 x
+(8192*N), one y slab per GPU (process), halos (north / south rows only) over
+RCCL.  Slabs rather than the reference's 2-D partitionForIpus blocks (1x2,
+2x2, 2x4, kept for config 4 below): the strip kernel walks rows, so a cut in
+x leaves 4-column boundary strips that cost nearly a full strip each -- on
+one GPU 4 slabs run 243 GLUPS against 192 for 2x2 blocks and 8 slabs 235
+against 223 for 2x4 (profiles/r01/stream/ab_parts_weak.log).  Rank 0 at N=1 also runs BASELINE config 2 (the
 reference 1024x1024 problem, 20 000 steps) and the CPU baseline.  Every N
 also reports, under "aux": config 4 (the fixed 16384x16384 grid split over
 all ranks: strong scaling) and config 5 (D3Q19 512^3 in z slabs over all
@@ -76,7 +80,8 @@ def synthetic_obstacles(nx: int, ny: int) -> np.ndarray:
 
 
 def weak_grid(n: int):
-    return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}[n]
+    """(rows, columns) of per-GPU tiles: y slabs (see the module docstring)."""
+    return (n, 1)
 
 
 def log(msg: str) -> None:
@@ -350,7 +355,7 @@ def main() -> int:
         "data": "synthetic (deterministic obstacles: border walls + interior column at x=nx/3; equilibrium start)",
         "config": {"workload": f"D2Q9-BGK fused step, {tnx}x{tny} fp32 cells per GPU",
                    "global_grid": f"{nx}x{ny}", "decomposition": f"{R}x{C}",
-                   "parallelism": "2-D block decomposition, RCCL halo exchange" if n > 1 else "single GPU",
+                   "parallelism": f"{n} y slabs, one per GPU, RCCL halo exchange" if n > 1 else "single GPU",
                    "kernel": kernel_used},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

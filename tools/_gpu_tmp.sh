@@ -2,10 +2,5 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
-  "900|pytest_gpu|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
-  "300|smoke|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "400|bench|python bench.py" \
-  "300|prof_trace|rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o bench --output-format csv -- python3 bench.py --steps 400 --no-cpu-baseline --no-aux" \
-  "120|pmc_fetch|timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1" \
-  "120|pmc_write|timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1"
-grep -h "passed\|failed" gpurun_out/pytest_gpu.log; tail -2 gpurun_out/smoke.log; tail -1 gpurun_out/bench.log
+  "500|weak|python tools/ab_parts.py --tile 8192 --grids 1x1 1x2 2x1 2x2 4x1 2x4 8x1 --steps 100"
+grep -h mlups gpurun_out/weak.log
