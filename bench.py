@@ -174,9 +174,12 @@ def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
 
 def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on: bool) -> dict:
     """BASELINE config 4: the fixed 16384x16384 grid (synthetic obstacles) over all
-    ranks -- 2-D blocks by the reference's partitionForIpus rule (1x1, 1x2, 2x2,
-    2x4), RCCL halos overlapped with the interior -- whole-job MLUPS (strong
-    scaling; the target is >= 6x at 8 GPUs over 1)."""
+    ranks, RCCL halos overlapped with the interior -- whole-job MLUPS (strong
+    scaling; the target is >= 6x at 8 GPUs over 1).  Split into y slabs (N x 1)
+    rather than the reference's partitionForIpus blocks (1x2, 2x2, 2x4, the
+    engine's default and lbm_partition's answer): emulated on one GPU, 2/4/8
+    slabs ran 250/246/202 GLUPS against 200/199/182 for the blocks
+    (profiles/r01/stream/ab_parts_strong.log)."""
     import torch.distributed as dist
     n = 16384
     p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
@@ -185,7 +188,8 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
     if dist_on:
         box = [native.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-        kw.update(parts=world, transport=native.TRANSPORT_RCCL, rank=rank, world=world, unique_id=box[0])
+        kw.update(parts=world, grid=(world, 1), transport=native.TRANSPORT_RCCL, rank=rank, world=world,
+                  unique_id=box[0])
     with native.Engine(p, obst, **kw) as e:
         e.init_equilibrium()
         e.run_steps(8, accelerate_first=True)
@@ -203,7 +207,8 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
         t = torch.tensor([secs], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         secs = float(t[0])
-    return {"grid": f"{n}x{n}", "steps": steps, "sub_domain": f"{rect[2]}x{rect[3]}", "kernel": kernel_used,
+    return {"grid": f"{n}x{n}", "steps": steps, "decomposition": f"{world}x1 (y slabs)",
+            "sub_domain": f"{rect[2]}x{rect[3]}", "kernel": kernel_used,
             "mlups": round(n * n * steps / secs / 1e6, 1), "ms_per_step": round(secs / steps * 1e3, 4)}
 
 
