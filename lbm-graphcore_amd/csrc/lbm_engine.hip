@@ -561,8 +561,13 @@ struct lbm_handle {
         auto ow_of = [&](int rx) { return stream_v == 1 ? 64 - 2 * S : (((rx - S) & 1) ? 126 - 2 * S : 128 - 2 * S); };
         const bool xdec = s.remote[DE] || s.remote[DW];
         const bool ydec = s.remote[DN] || s.remote[DS];
+        // a decomposed x side's boundary band is one whole strip wide when the
+        // sub-domain has room: an S-column band costs nearly a full strip per
+        // segment for S useful columns (tools/ab_parts.py)
+        const int ow_min = stream_v == 1 ? 64 - 2 * S : 126 - 2 * S;
+        const int xb = (xdec && s.w >= 4 * ow_min) ? ow_min : b;
         const int y0 = ydec ? b : 0, y1 = ydec ? s.h - b : s.h;
-        const int x0 = xdec ? b : 0, x1 = xdec ? s.w - b : s.w;
+        const int x0 = xdec ? xb : 0, x1 = xdec ? s.w - xb : s.w;
         int hs = stream_hs;
         if (hs <= 0) {
             const long long strips = (std::max(x1 - x0, 1) + ow_of(x0) - 1) / ow_of(x0);
@@ -600,8 +605,8 @@ struct lbm_handle {
             bnd.push_back(mk(0, s.h - b, s.w, b, b));
         }
         if (xdec && y1 > y0) {
-            bnd.push_back(mk(0, y0, b, y1 - y0, hs));
-            bnd.push_back(mk(s.w - b, y0, b, y1 - y0, hs));
+            bnd.push_back(mk(0, y0, xb, y1 - y0, hs));
+            bnd.push_back(mk(s.w - xb, y0, xb, y1 - y0, hs));
         }
         if (x1 > x0 && y1 > y0) inr.push_back(mk(x0, y0, x1 - x0, y1 - y0, hs));
     }
