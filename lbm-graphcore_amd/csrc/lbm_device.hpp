@@ -195,10 +195,11 @@ struct RectPos {
 
 // Tile t (BLOCK work items, wave-uniform) -> rect; lane -> (column chunk, row).
 // Every tile lies inside one rect, so the rect lookup stays scalar.
-__device__ __forceinline__ int rect_of(const int (&rect_begin)[MAX_RECTS], int t) {
+template <int N>
+__device__ __forceinline__ int rect_of(const int (&rect_begin)[N], int t) {
     int r = 0;
 #pragma unroll
-    for (int i = 1; i < MAX_RECTS; ++i) r = (t >= rect_begin[i]) ? i : r;
+    for (int i = 1; i < N; ++i) r = (t >= rect_begin[i]) ? i : r;
     return __builtin_amdgcn_readfirstlane(r);
 }
 

@@ -46,6 +46,8 @@ hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t
 hipError_t launch_stream(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
 hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s);
 hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n);
+hipError_t launch_stream2d(const StreamArgs &a, int blocks, int steps, bool reduce, int pd, hipStream_t s);
+hipError_t stream2d_blocks_per_cu(int steps, int pd, int &n);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
@@ -169,6 +171,8 @@ struct Sub {
     int n3_int = 0, n3_bnd = 0;             // stream launch block counts
     int cur = 0;                            // lattice holding the current state
     float *pipe_partials = nullptr;         // PIPELINE: collision block partials
+    Dst2 *dst2_dev = nullptr;               // [parity][8] stream-kernel halo destinations (StreamArgs::dstg)
+    unsigned long long *trace = nullptr;    // LBM_STREAM_TRACE: per-wave timestamps of the last interior launch
 };
 
 }  // namespace
@@ -186,9 +190,12 @@ struct lbm_handle {
     int gr = 2;              // ghost ring width
     int stream_s = 4;        // LBM_STREAM_S: steps per stream launch when not configured
     int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
-    int stream_v = 2;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32)
+    int stream_v = 2;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32),
+                             // 3 = two columns per lane without the streaming order's redundant work
     int og = 4;              // ghost width of the obstacle map
+    std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     int stream_waves = 2;    // LBM_STREAM_W: register target of the two-column kernel (waves per SIMD)
+    int stream_pd = 2;       // LBM_STREAM_PD: v3 prefetch distance in rows (1 or 2)
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
@@ -249,9 +256,28 @@ struct lbm_handle {
         xoff = std::max(MAX_GR, (env_int("LBM_XOFF", xoff) + 3) / 4 * 4);
         stream_s = std::min(std::max(env_int("LBM_STREAM_S", stream_s), 2), 4);
         stream_hs = std::max(0, env_int("LBM_STREAM_HS", stream_hs));
-        stream_v = env_int("LBM_STREAM_V", stream_v) == 1 ? 1 : 2;
+        stream_v = std::min(std::max(env_int("LBM_STREAM_V", stream_v), 1), 3);
         stream_waves = env_int("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
+        stream_pd = env_int("LBM_STREAM_PD", stream_pd) == 1 ? 1 : 2;
         stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
+        {
+            const char *g = getenv("LBM_STREAM_GUIDE");
+            std::string spec = g ? std::string(g) : std::string("72:0.85,24:0.1,8");
+            guide.clear();
+            if (spec != "0") {
+                size_t pos = 0;
+                while (pos < spec.size()) {
+                    size_t end = spec.find(',', pos);
+                    if (end == std::string::npos) end = spec.size();
+                    const std::string item = spec.substr(pos, end - pos);
+                    const size_t c = item.find(':');
+                    const int ht = atoi(item.substr(0, c).c_str());
+                    const float fr = c == std::string::npos ? 1.f : (float)atof(item.substr(c + 1).c_str());
+                    if (ht > 0) guide.emplace_back(ht, fr);
+                    pos = end + 1;
+                }
+            }
+        }
         res_th_env = std::max(0, env_int("LBM_RES_TH", 0));
         res_version = env_int("LBM_RES_V", 0);
         res_per_cu = std::min(std::max(env_int("LBM_RES_PER_CU", res_per_cu), 1), 2);
@@ -542,6 +568,13 @@ struct lbm_handle {
                 a->n_total = n3;
                 a->stride = st3;
             }
+            if (!s.dst2_dev) HIP_CHECK(hipMalloc(&s.dst2_dev, sizeof(Dst2) * 16));
+            HIP_CHECK(hipMemcpy(s.dst2_dev + 8 * par, si.dst, sizeof(Dst2) * 8, hipMemcpyHostToDevice));
+            si.dstg = sb.dstg = s.dst2_dev + 8 * par;
+            if (getenv("LBM_STREAM_TRACE") && use_stream && s.n3_int > 0) {
+                if (!s.trace) HIP_CHECK(hipMalloc(&s.trace, sizeof(unsigned long long) * 2 * (size_t)s.n3_int));
+                si.trace = s.trace;
+            }
             si.partials_out = s.partials[par];
             sb.partials_out = s.partials[par] + s.n3_int;
             s.a3_int[par] = si;
@@ -580,7 +613,9 @@ struct lbm_handle {
             // (profiles/r01/stream/ab_hs_rounds.log).  Eight rounds where the
             // segments stay at least 4S rows high, fewer otherwise.
             int per_cu = 0, cus = 0;
-            if (stream_v == 2 && stream2c_blocks_per_cu(S, stream_waves, per_cu) == hipSuccess &&
+            const hipError_t occ = stream_v == 3 ? stream2d_blocks_per_cu(S, stream_pd, per_cu)
+                                                 : stream2c_blocks_per_cu(S, stream_waves, per_cu);
+            if (stream_v >= 2 && occ == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev) == hipSuccess &&
                 per_cu > 0 && cus > 0) {
                 const long long cap = (long long)per_cu * cus;
@@ -608,13 +643,48 @@ struct lbm_handle {
             bnd.push_back(mk(0, y0, xb, y1 - y0, hs));
             bnd.push_back(mk(s.w - xb, y0, xb, y1 - y0, hs));
         }
-        if (x1 > x0 && y1 > y0) inr.push_back(mk(x0, y0, x1 - x0, y1 - y0, hs));
+        if (x1 > x0 && y1 > y0) {
+            if (!guided_rects(x0, y0, x1 - x0, y1 - y0, mk, inr)) inr.push_back(mk(x0, y0, x1 - x0, y1 - y0, hs));
+        }
+    }
+
+    // Guided segment heights for the interior of the stream launch (auto
+    // heights only).  Waves of one launch differ in duration by +-10-15 %
+    // (tools/stream_trace.py), so equal segments leave the device's slots
+    // idling while the last ones finish; instead the rows are cut into one
+    // band per XCD (blocks b and b+8 share an XCD and are dispatched in b
+    // order, xcd_remap gives each XCD a contiguous range of work units), and
+    // each band into tiers of decreasing segment height: tall segments
+    // (little re-streamed overlap) first, short ones last to fill the tail.
+    // LBM_STREAM_GUIDE = "h1:f1,h2:f2,...,hK" (tier heights, fractions of a
+    // band's rows; the last tier takes the rest), "0" = uniform heights.
+    template <class MK>
+    bool guided_rects(int x0, int y0, int w, int h, MK &&mk, std::vector<SRect> &out) const {
+        if (stream_hs > 0 || stream_v < 2 || guide.empty()) return false;
+        constexpr int NB = 8;
+        const int hb = h / NB;
+        if (hb < 2 * guide[0].first) return false;
+        const auto rows = round_robin(h, NB);
+        int y = y0;
+        for (int band = 0; band < NB; ++band) {
+            int rest = rows[band];
+            for (size_t k = 0; k < guide.size() && rest > 0; ++k) {
+                const int ht = std::max(1, guide[k].first);
+                int r = rest;
+                if (k + 1 < guide.size()) r = std::min(rest, std::max(ht, (int)(rows[band] * guide[k].second) / ht * ht));
+                out.push_back(mk(x0, y, w, r, ht));
+                y += r;
+                rest -= r;
+            }
+        }
+        return (int)out.size() <= MAX_SRECTS;
     }
 
     int fill_srects(StreamArgs &a, const std::vector<SRect> &rs) const {
         int units = 0;
         a.nrect = (int)rs.size();
-        for (int i = 0; i < MAX_RECTS; ++i) {
+        if (a.nrect > MAX_SRECTS) throw lbm_failure(LBM_E_INTERNAL, "too many stream rects");
+        for (int i = 0; i < MAX_SRECTS; ++i) {
             if (i < a.nrect) {
                 a.rect[i] = rs[i];
                 a.rect_begin[i] = units;
@@ -1198,8 +1268,9 @@ struct lbm_handle {
             const int n = interior ? s.n3_int : s.n3_bnd;
             if (n <= 0) return hipSuccess;
             const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
-            return stream_v == 1 ? launch_stream(a, n, spl, interior, st)
-                                 : launch_stream2c(a, n, spl, interior, stream_waves, st);
+            if (stream_v == 1) return launch_stream(a, n, spl, interior, st);
+            if (stream_v == 3) return launch_stream2d(a, n, spl, interior, stream_pd, st);
+            return launch_stream2c(a, n, spl, interior, stream_waves, st);
         }
         if (fused_launch) {
             const int n = interior ? s.n2_int : s.n2_bnd;
@@ -1372,6 +1443,22 @@ struct lbm_handle {
         last_seconds = ms * 1e-3;
         last_steps = steps;
         sync_all();
+        dump_trace();
+    }
+
+    // LBM_STREAM_TRACE=<file>: raw {start, end} s_memrealtime (100 MHz) per
+    // block of sub-domain 0's last interior stream launch (tools/stream_trace.py)
+    void dump_trace() {
+        const char *path = getenv("LBM_STREAM_TRACE");
+        if (!path || !*path || subs.empty() || !subs[0].trace) return;
+        Sub &s = subs[0];
+        set_device(s);
+        std::vector<unsigned long long> v(2 * (size_t)s.n3_int);
+        HIP_CHECK(hipMemcpy(v.data(), s.trace, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (FILE *f = fopen(path, "wb")) {
+            fwrite(v.data(), sizeof(unsigned long long), v.size(), f);
+            fclose(f);
+        }
     }
 
     void sync_all() {
@@ -1474,6 +1561,8 @@ struct lbm_handle {
             }
             if (s.obst) (void)hipFree(s.obst);
             if (s.pipe_partials) (void)hipFree(s.pipe_partials);
+            if (s.dst2_dev) (void)hipFree(s.dst2_dev);
+            if (s.trace) (void)hipFree(s.trace);
             if (s.obst_g) (void)hipFree(s.obst_g);
             if (s.halo_mem) (void)hipFree(s.halo_mem);
             if (s.av_local) (void)hipFree(s.av_local);

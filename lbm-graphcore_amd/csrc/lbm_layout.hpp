@@ -37,6 +37,7 @@ constexpr int XOFF = 4;   // interior column 0 offset inside a plane row
 constexpr int MAX_GR = 4;  // widest ghost ring (rows/columns) any kernel needs
 constexpr int BLOCK = 256;  // 4 wave64s
 constexpr int MAX_RECTS = 4;
+constexpr int MAX_SRECTS = 32;  // stream kernels: guided per-XCD row bands (lbm_engine.hip stream_split)
 
 // fused two-step tile shapes (cells).  v1 (step2): LDS intermediate
 // 9 x (TH+2) x (TW+2) floats, 256 threads.  v2 (step2w): one wave per tile
@@ -156,9 +157,11 @@ struct StreamArgs {
     int gy0, ny, accel_g;
     float omega, omo, w1, w2;
     int nrect, total;       // total work units (strip x segment)
-    SRect rect[MAX_RECTS];
-    int rect_begin[MAX_RECTS];
+    SRect rect[MAX_SRECTS];
+    int rect_begin[MAX_SRECTS];
     Dst2 dst[8];            // WG halo destinations, g = S
+    const Dst2 *dstg;       // the same eight in device memory (read only where a halo cell is stored)
+    unsigned long long *trace;  // diagnostics (LBM_STREAM_TRACE): per unit {start, end} s_memrealtime, or null
     float *partials_out;    // step s of this launch: partials_out[s*stride + blockIdx.x]
     const float *partials_prev;
     float *av_local;

@@ -122,4 +122,54 @@ __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bo
     return f2{oa ? 0.f : sqrt_av(usq.x), ob ? 0.f : sqrt_av(usq.y)};
 }
 
+// collide2 for a wave whose pair row is uniform: the folded acceleration is
+// applied only on the accelerated row (accrow, wave-uniform) exactly as
+// LastChance.cpp:253-261 does, and |u|^2 is returned for the caller to take
+// the square root only where the row counts towards av_vels.
+__device__ __forceinline__ f2 collide2u(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, bool accrow,
+                                        float omega, float omo, float w1, float w2) {
+    const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
+    f2 ux, uy;
+    div_pair(s[1] + s[5] + s[8] - (s[3] + s[6] + s[7]), s[2] + s[5] + s[6] - (s[4] + s[7] + s[8]), rho, ux, uy);
+    const f2 usq = ux * ux + uy * uy;
+    const f2 csq = mk2(1.00f) - usq * mk2(1.50f);
+    const f2 ld1 = div_const<9>(rho) * mk2(omega);
+    const f2 ld2 = div_const<36>(rho) * mk2(omega);
+    const f2 OMO = mk2(omo);
+    const f2 c23 = mk2(2.00f / 3.00f);
+    const f2 c45 = mk2(4.50f), n45 = mk2(-4.50f);
+
+    f2 c[Q];
+    c[0] = s[0] * OMO + mk2(4.00f / 9.00f) * rho * mk2(omega) * csq;
+    c[1] = s[1] * OMO + ld1 * ((c45 * ux) * (c23 + ux) + csq);
+    c[3] = s[3] * OMO + ld1 * ((n45 * ux) * (c23 - ux) + csq);
+    c[2] = s[2] * OMO + ld1 * ((c45 * uy) * (c23 + uy) + csq);
+    c[4] = s[4] * OMO + ld1 * ((n45 * uy) * (c23 - uy) + csq);
+    const f2 us = ux + uy;
+    c[5] = s[5] * OMO + ld2 * ((c45 * us) * (c23 + us) + csq);
+    c[7] = s[7] * OMO + ld2 * ((n45 * us) * (c23 - us) + csq);
+    const f2 ud = -ux + uy;
+    c[6] = s[6] * OMO + ld2 * ((c45 * ud) * (c23 + ud) + csq);
+    c[8] = s[8] * OMO + ld2 * ((n45 * ud) * (c23 - ud) + csq);
+    if (accrow) {
+        const f2 a1 = mk2(w1), a2 = mk2(w2);
+        c[1] = c[1] + a1;
+        c[3] = c[3] - a1;
+        c[5] = c[5] + a2;
+        c[6] = c[6] - a2;
+        c[7] = c[7] - a2;
+        c[8] = c[8] + a2;
+    }
+    if (!any_obst) {
+#pragma unroll
+        for (int k = 0; k < Q; ++k) o[k] = c[k];
+        return usq;
+    }
+    // obstacle cells rebound: out_k = s_opp(k)
+    constexpr int OPP[Q] = {0, 3, 4, 1, 2, 7, 8, 5, 6};
+#pragma unroll
+    for (int k = 0; k < Q; ++k) o[k] = f2{oa ? s[OPP[k]].x : c[k].x, ob ? s[OPP[k]].y : c[k].y};
+    return usq;
+}
+
 }  // namespace lbm

@@ -176,6 +176,266 @@ __global__ __launch_bounds__(64, MINW) void stream_steps2c(StreamArgs a) {
     if (kReduce && blockIdx.x == 0 && lane == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
 }
 
+// halo_out with the destinations read from device memory inside the (rare)
+// branch that stores them, so they hold no scalar registers across the loop
+__device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, int y, const float (&o)[Q]) {
+    const bool east = x >= a.w - S, west = x < S, north = y >= a.h - S, south = y < S;
+    const Dst2 *dg = a.dstg;
+    if (east) store2(dg[DE], x - (a.w - S), y, o);
+    if (west) store2(dg[DW], x, y, o);
+    if (north) {
+        store2(dg[DN], y - (a.h - S), x, o);
+        if (east) store2(dg[DNE], y - (a.h - S), x - (a.w - S), o);
+        if (west) store2(dg[DNW], y - (a.h - S), x, o);
+    }
+    if (south) {
+        store2(dg[DS], y, x, o);
+        if (west) store2(dg[DSW], y, x, o);
+        if (east) store2(dg[DSE], y, x - (a.w - S), o);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// stream_steps2d: the same schedule and arithmetic as stream_steps2c with the
+// work the streaming order makes redundant removed (every lattice value and
+// every |u| partial bitwise unchanged):
+//   * level L's first 2L row iterations of a segment would compute rows whose
+//     own inputs were never loaded (their results are never used): they are
+//     skipped (a warm-up loop of 2S iterations with wave-uniform guards, then
+//     a guard-free main loop);
+//   * the row loop is unrolled by two with the rows y-1 / y of planes 2, 5, 6
+//     in parity-alternating registers, so the row rotation costs no moves;
+//   * the folded acceleration is applied on the accelerated row only (a
+//     wave-uniform branch, as LastChance.cpp:253-261) instead of adding zero
+//     everywhere else;
+//   * |u| (a v_sqrt per cell) only for rows that count towards av_vels;
+//   * one ballot per loaded row (not per level) tells whether any obstacle
+//     cell is in it.
+template <int S>
+struct Stream2State {
+    f2 c0[S], c1[S], c3[S];          // planes 0, 1, 3 of row y (level L input)
+    f2 p2[2][S], p5[2][S], p6[2][S]; // [parity]: planes 2, 5(left2), 6(right2) of rows y-1 / y
+    f2 tot[S];
+    f2 v[2][Q];                      // [parity]: input row j (parity of j) / prefetched row j+1
+    unsigned ob[2][2];               // [parity][A/B]: obstacle bytes of those rows
+    unsigned oba, obb;               // per-lane obstacle bits of the last rows (bit L = row j-L)
+    unsigned long long rob;          // wave-uniform: bit L = row j-L has an obstacle cell
+};
+
+struct Stream2Geo {
+    const float *src;
+    const uint8_t *obp;
+    long long P;
+    int pitch, xa, xb, yo0, yo1, j0, jlast;
+    bool owna, ownb;
+};
+
+// Prefetch distance PD: the loads of row j+PD (clamped to the segment) are
+// issued while row j is computed -- PD = 2 keeps two rows of every wave in
+// flight (the kernel is bound by the memory-level parallelism of two waves
+// per SIMD, not by VALU: tools/pmc_summary.py SQ_WAIT_ANY), at 18 more VGPRs.
+template <int PD>
+__device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2Geo &g, int j, f2 (&v)[Q],
+                                              unsigned (&ob)[2]) {
+    const int jn = min(j, g.jlast);
+    const float *cn = g.src + (long long)jn * g.pitch;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const f2 *>(cn + k * g.P);
+    const uint8_t *ocn = g.obp + (long long)(jn + a.og) * a.ogp;
+    ob[0] = ocn[0];
+    ob[1] = ocn[1];
+}
+
+template <int S, int PAR, bool GUARD, int PD>
+__device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j) {
+    // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
+    if (PD == 1) stream2d_load<PD>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
+    const unsigned voa = st.ob[PAR][0] != 0 ? 1u : 0u, vob = st.ob[PAR][1] != 0 ? 1u : 0u;
+    st.oba = (st.oba << 1) | voa;
+    st.obb = (st.obb << 1) | vob;
+    st.rob = (st.rob << 1) | (__builtin_amdgcn_ballot_w64((voa | vob) != 0) != 0 ? 1ull : 0ull);
+
+    f2 cur[Q];
+#pragma unroll
+    for (int k = 0; k < Q; ++k) cur[k] = st.v[PAR][k];
+    if (PD == 2) stream2d_load<PD>(a, g, j + 2, st.v[PAR], st.ob[PAR]);
+#pragma unroll
+    for (int L = 1; L <= S; ++L) {
+        const int b = L - 1;
+        const int y = j - L;
+        // pulled populations of row y (level L-1 values; x +- 1 by DPP)
+        const f2 s[Q] = {st.c0[b],    st.c1[b],           st.p2[PAR][b],     st.c3[b], cur[4],
+                         st.p5[PAR][b], st.p6[PAR][b], right2(cur[7]), left2(cur[8])};
+        st.p2[PAR][b] = cur[2];
+        st.p5[PAR][b] = left2(cur[5]);
+        st.p6[PAR][b] = right2(cur[6]);
+        st.c0[b] = cur[0];
+        st.c1[b] = left2(cur[1]);
+        st.c3[b] = right2(cur[3]);
+        if (GUARD && j < g.j0 + 2 * L) continue;  // inputs of this row were never loaded: result unused
+
+        f2 o[Q];
+        const bool oa = (st.oba >> L) & 1u, ob = (st.obb >> L) & 1u;
+        const bool any_obst = (st.rob >> L) & 1ull;
+        int gy = a.gy0 + y;
+        gy = gy < 0 ? gy + a.ny : (gy >= a.ny ? gy - a.ny : gy);
+        const f2 usq = collide2u(s, o, oa, ob, any_obst, gy == a.accel_g, a.omega, a.omo, a.w1, a.w2);
+        const bool rowlive = (!GUARD || y >= g.yo0) && (L == S || y < g.yo1);
+        if (rowlive) {
+            const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
+            const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
+            st.tot[b] += f2{ua, ub};
+        }
+        if (L == S) {
+            if (rowlive && (g.owna || g.ownb)) {
+                float *w0 = a.fout + (long long)y * g.pitch + g.xa;
+                if (g.owna && g.ownb) {
+#pragma unroll
+                    for (int k = 0; k < Q; ++k) *reinterpret_cast<f2 *>(w0 + k * g.P) = o[k];
+                } else if (g.owna) {
+#pragma unroll
+                    for (int k = 0; k < Q; ++k) w0[k * g.P] = o[k].x;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < Q; ++k) w0[k * g.P + 1] = o[k].y;
+                }
+                if (g.xa < S || g.xb >= a.w - S || y < S || y >= a.h - S) {
+                    float oa_[Q], ob_[Q];
+#pragma unroll
+                    for (int k = 0; k < Q; ++k) {
+                        oa_[k] = o[k].x;
+                        ob_[k] = o[k].y;
+                    }
+                    if (g.owna) halo_out_g(a, S, g.xa, y, oa_);
+                    if (g.ownb) halo_out_g(a, S, g.xb, y, ob_);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < Q; ++k) cur[k] = o[k];
+        }
+    }
+}
+
+// One work unit (strip x segment t) of the launch; accumulates |u| per level into st.tot.
+template <int S, int PD>
+__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st) {
+    const int r = rect_of(a.rect_begin, t);
+    const SRect R = a.rect[r];
+    const int lt = t - a.rect_begin[r];
+    const int seg = lt / R.nstrip, strip = lt - seg * R.nstrip;
+    const int xo0 = R.x0 + strip * R.ow;             // first owned column
+    const int xo1 = min(xo0 + R.ow, R.x0 + R.w);     // past the last owned column
+    const int base = (xo0 - S) & ~1;                 // even: float2-aligned
+    Stream2Geo g;
+    g.xa = base + 2 * lane;
+    g.xb = g.xa + 1;
+    g.owna = g.xa >= xo0 && g.xa < xo1;
+    g.ownb = g.xb >= xo0 && g.xb < xo1;
+    g.yo0 = R.y0 + seg * R.hs;
+    g.yo1 = min(g.yo0 + R.hs, R.y0 + R.h);
+    const int xca = min(g.xa, (a.xmax - 1) & ~1);
+    g.P = a.plane;
+    g.pitch = a.pitch;
+    g.src = a.fin + xca;
+    g.obp = a.obst_g + (xca + a.og);
+    g.j0 = g.yo0 - S;
+    g.jlast = g.yo1 + S - 1;
+
+#pragma unroll
+    for (int b = 0; b < S; ++b) {
+        st.c0[b] = st.c1[b] = st.c3[b] = mk2(0.f);
+        st.p2[0][b] = st.p5[0][b] = st.p6[0][b] = st.p2[1][b] = st.p5[1][b] = st.p6[1][b] = mk2(0.f);
+    }
+    st.oba = st.obb = 0;
+    st.rob = 0;
+    stream2d_load<PD>(a, g, g.j0, st.v[0], st.ob[0]);
+    if (PD == 2) stream2d_load<PD>(a, g, g.j0 + 1, st.v[1], st.ob[1]);
+    // warm-up: rows j0 .. j0+2S-1 (level L valid from j0+2L); jlast >= j0+2S
+    int j = g.j0;
+#pragma unroll 1
+    for (int i = 0; i < S; ++i, j += 2) {
+        stream2d_row<S, 0, true, PD>(a, g, st, j);
+        stream2d_row<S, 1, true, PD>(a, g, st, j + 1);
+    }
+#pragma unroll 1
+    for (; j + 1 <= g.jlast; j += 2) {
+        stream2d_row<S, 0, false, PD>(a, g, st, j);
+        stream2d_row<S, 1, false, PD>(a, g, st, j + 1);
+    }
+    if (j <= g.jlast) stream2d_row<S, 0, false, PD>(a, g, st, j);
+}
+
+// |u| partials of one work unit, one per level (= time step of the launch)
+template <int S>
+__device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, int lane, Stream2State<S> &st) {
+#pragma unroll
+    for (int l = 0; l < S; ++l) {
+        float sum = st.tot[l].x + st.tot[l].y;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
+        if (lane == 0) a.partials_out[(long long)l * a.stride + idx] = sum;
+        st.tot[l] = mk2(0.f);
+    }
+}
+
+// One work unit per wave, t = xcd_remap(blockIdx) (blocks b and b+8 share an
+// XCD and take neighbouring units, so the strips' overlap columns are read
+// through one L2).  (A persistent grid taking units from a device-scope
+// counter balanced the waves better but read 1.30x the algorithmic bytes
+// instead of 1.18x: neighbouring strips landed on different XCDs.)
+template <int S, bool kReduce, int PD, int MINW>
+__global__ __launch_bounds__(64, MINW) void stream_steps2d(StreamArgs a) {
+    __shared__ float lds[1];
+    if (kReduce && blockIdx.x == 0) reduce_pending_n<64>(a.ctl, a.partials_prev, a.av_local, lds);
+
+    const int lane = threadIdx.x;
+    Stream2State<S> st;
+#pragma unroll
+    for (int l = 0; l < S; ++l) st.tot[l] = mk2(0.f);
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    if (t < a.total) stream2d_unit<S, PD>(a, t, lane, st);
+    stream2d_partials<S>(a, blockIdx.x, lane, st);
+    if (a.trace && lane == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        a.trace[2 * (long long)blockIdx.x] = t_start;
+        a.trace[2 * (long long)blockIdx.x + 1] = t_end;
+    }
+    if (kReduce && blockIdx.x == 0 && lane == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
+}
+
+template <int S, int PD>
+static void launch_s2d(const StreamArgs &a, int blocks, bool reduce, hipStream_t s) {
+    if (reduce)
+        hipLaunchKernelGGL((stream_steps2d<S, true, PD, 2>), dim3(blocks), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((stream_steps2d<S, false, PD, 2>), dim3(blocks), dim3(64), 0, s, a);
+}
+
+hipError_t stream2d_blocks_per_cu(int steps, int pd, int &n) {
+    const void *fn = pd == 2 ? (steps == 2   ? (const void *)&stream_steps2d<2, false, 2, 2>
+                                : steps == 3 ? (const void *)&stream_steps2d<3, false, 2, 2>
+                                             : (const void *)&stream_steps2d<4, false, 2, 2>)
+                             : (steps == 2   ? (const void *)&stream_steps2d<2, false, 1, 2>
+                                : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, 2>
+                                             : (const void *)&stream_steps2d<4, false, 1, 2>);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, 0);
+}
+
+hipError_t launch_stream2d(const StreamArgs &a, int blocks, int steps, bool reduce, int pd, hipStream_t s) {
+    switch (steps * 10 + pd) {
+        case 21: launch_s2d<2, 1>(a, blocks, reduce, s); break;
+        case 31: launch_s2d<3, 1>(a, blocks, reduce, s); break;
+        case 41: launch_s2d<4, 1>(a, blocks, reduce, s); break;
+        case 22: launch_s2d<2, 2>(a, blocks, reduce, s); break;
+        case 32: launch_s2d<3, 2>(a, blocks, reduce, s); break;
+        case 42: launch_s2d<4, 2>(a, blocks, reduce, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <int S, int MINW>
 static void launch_s2c(const StreamArgs &a, int blocks, bool reduce, hipStream_t s) {
     if (reduce)

@@ -32,9 +32,14 @@ from bench import synthetic_obstacles  # noqa: E402
 def parse_variant(s: str):
     name, _, rest = s.partition(":")
     env = {}
+    last = None
     for kv in filter(None, rest.split(",")):
+        if "=" not in kv and last is not None:  # a value that itself contains commas
+            env[last] += "," + kv
+            continue
         k, _, v = kv.partition("=")
         env[k] = v
+        last = k
     return name, env
 
 
