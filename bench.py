@@ -11,21 +11,26 @@ Workload (config.workload): BASELINE config 3, 8192x8192 fp32 cells per GPU
 with deterministic synthetic obstacles (walls on the four borders plus one
 full interior column at x = nx/3, mimicking obstacles_1024x1024.dat), rho 0.1,
 accel 0.005, omega 1.85, equilibrium start.  For N > 1 the per-GPU tile is
-fixed (weak scaling): the tiles are stacked in y, global grid 8192 x
-(8192*N), one y slab per GPU (process), halos (north / south rows only) over
-RCCL.  Slabs rather than the reference's 2-D partitionForIpus blocks (1x2,
-2x2, 2x4, kept for config 4 below): the strip kernel walks rows, so a cut in
-x leaves 4-column boundary strips that cost nearly a full strip each -- on
-one GPU 4 slabs run 243 GLUPS against 192 for 2x2 blocks and 8 slabs 235
-against 223 for 2x4 (profiles/r01/stream/ab_parts_weak.log).  Rank 0 at N=1 also runs BASELINE config 2 (the
-reference 1024x1024 problem, 20 000 steps) and the CPU baseline.  Every N
-also reports, under "aux": config 4 (the fixed 16384x16384 grid split over
-all ranks: strong scaling) and config 5 (D3Q19 512^3 in z slabs over all
-ranks).  Why 8192^2 per GPU is `value` although the metric also names 1024^2:
-it is the HBM-roofline configuration (config 3, inputs resident in HBM, 4.8 GB
-of lattice traffic per step) and the one that weak-scales to N GPUs; the
-1024^2 reference problem runs on chip (resident kernel) and is reported as
-aux.config2_1024x1024.
+fixed (weak scaling) and the tiles are arranged by the reference's
+partitionForIpus rule (StructuredGridUtils.hpp:498-522: 1x2, 2x2, 2x4 for a
+square tile; rank = row*cols + col), one sub-domain per GPU (process), halos
+over RCCL -- the 2-D blocks north_star names.  aux.weak_slabs runs the same
+per-GPU tile as N x 1 y slabs (north/south halos only) for comparison.
+Rank 0 at N=1 also runs BASELINE config 2 (the reference 1024x1024 problem,
+20 000 steps) and the CPU baselines.  Every N also reports, under "aux":
+config 4 (the fixed 16384x16384 grid split over all ranks by the reference
+rule; strong scaling) and the same as y slabs (config4_slabs, N > 1), and
+config 5 (D3Q19 512^3 in z slabs over all ranks).  Why 8192^2 per GPU is
+`value` although the metric also names 1024^2: it is the HBM-roofline
+configuration (config 3, inputs resident in HBM, 4.8 GB of lattice traffic
+per step) and the one that weak-scales to N GPUs; the 1024^2 reference
+problem runs on chip (resident kernel) and is reported as aux.config2_1024x1024.
+
+Settling: the GPU ramps its clock for the first ~20-30 ms of back-to-back
+work (tools/settle_probe.py: a 20-step run right after a 5-step warm-up took
+1.38 ms per launch, the same run settled 1.20), so after the W warm-up steps
+the bench runs untimed "settle" steps worth >= 0.3 s of device time (the same
+count on every rank) and reports them in the JSON ("settle").
 
 Timed region: K steps between barrier + torch.cuda.synchronize() pairs, max
 over ranks.  value = all cells x K / seconds / 1e6 (whole job).
@@ -41,6 +46,17 @@ profiles/traffic.json (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when a
 profile of this workload + kernel exists, else null.  effective_gbs = 72 B x
 cell updates / s (SURVEY 8(d)'s MLUPS x 72 B form), which exceeds the HBM
 peak once temporal blocking pays.
+
+cpu_baseline: the reference's main/LbmCpu.cpp as committed (north_star: "next
+to LbmCpu.cpp timed on the same box's host cores"), built from its source by
+oracle/Makefile, on the 128x128 reference problem (all 40 000 steps, one
+thread: it has no OpenMP pragmas), timed by its own "Total compute time".  It
+is cost-only: its live kernel fails check.py upstream.
+aux.cpu_config1_128x128 is the config-1 plumbing record (LastChance.cpp, the
+reference's correct CPU path, full 128x128 run gated by check.py against the
+reference's check/ fixtures); aux.cpu_lastchance_1024x1024 a bounded sample
+of the 1024x1024 problem; aux.cpu_baseline_threads the restatement on every
+host core.
 """
 from __future__ import annotations
 
@@ -79,9 +95,20 @@ def synthetic_obstacles(nx: int, ny: int) -> np.ndarray:
     return o
 
 
-def weak_grid(n: int):
-    """(rows, columns) of per-GPU tiles: y slabs (see the module docstring)."""
-    return (n, 1)
+def weak_grid(n: int, tnx: int, tny: int, slabs: bool = False):
+    """(rows, columns) of per-GPU tiles: the reference rule for a tile-shaped
+    grid (lbm_partition = partitionForIpus), or N x 1 y slabs."""
+    if slabs or n == 1:
+        return (n, 1)
+    R, C, _ = native.partition(tnx, tny, n)
+    return (R, C)
+
+
+def settle_steps(per_step_s: float, spl: int, budget_s: float = 0.3) -> int:
+    """Untimed steps worth ~budget_s of device time (whole launches)."""
+    n = int(budget_s / max(per_step_s, 1e-7)) + 1
+    n = (n + spl - 1) // spl * spl
+    return max(spl, min(n, 20000))
 
 
 def log(msg: str) -> None:
@@ -102,33 +129,61 @@ def load_traffic(workload_key: str):
 
 
 def cpu_baseline() -> dict | None:
-    """The reference's own LastChance (oracle/_ref) on a bounded sample of the
-    1024x1024 reference problem, single thread on this host."""
-    from oracle import oracle  # checker / baseline only
+    """north_star's CPU baseline: main/LbmCpu.cpp as committed (oracle/_ref/lbm_cpu,
+    cost only), 128x128 reference problem, all 40 000 steps, one thread."""
+    from oracle import oracle  # baseline only
+    gold = ROOT / "tests" / "golden" / "params"
+    if not oracle.REF_LBMCPU.exists():
+        return None
+    with tempfile.TemporaryDirectory() as wd:
+        r = oracle.run_lbm_cpu(str(gold / "input_128x128.params"), str(gold / "obstacles_128x128.dat"), wd)
+    secs = r["compute_s"]
+    return {"value": round(128 * 128 * 40000 / secs / 1e6, 2),
+            "unit": "MLUPS", "cores": 1, "kind": "reference", "cpu_model": oracle.cpu_model(),
+            "sample": f"main/LbmCpu.cpp as committed (-O3, built from the reference source; cost only -- its live "
+                      f"kernel fails check.py upstream, SURVEY.md 8c), 128x128 reference problem, all 40000 steps, "
+                      f"its own 'Total compute time' {secs:.2f} s (includes its full-lattice printf), 1 thread of "
+                      f"{oracle.cpu_model()}"}
+
+
+def cpu_config1() -> dict | None:
+    """BASELINE config 1 plumbing: the reference's LastChance.cpp (correct CPU path)
+    on the full 128x128 reference problem, gated by check.py against check/*.dat."""
+    from oracle import oracle  # baseline only
+    from lbm_amd import check as lcheck
+    gold = ROOT / "tests" / "golden"
+    if not oracle.REF_LASTCHANCE.exists():
+        return None
+    with tempfile.TemporaryDirectory() as wd:
+        r = oracle.run_reference(str(gold / "params" / "input_128x128.params"),
+                                 str(gold / "params" / "obstacles_128x128.dat"), wd)
+        res = lcheck.compare(gold / "check" / "128x128.av_vels.dat.gz", gold / "check" / "128x128.final_state.dat.gz",
+                             r["av_vels"], r["final_state"])
+    secs = r["elapsed_s"]
+    return {"program": "main/LastChance.cpp (reference, compiled -O3 -ffp-contract=off)", "grid": "128x128",
+            "steps": 40000, "seconds": round(secs, 3), "mlups": round(128 * 128 * 40000 / secs / 1e6, 2),
+            "cores": 1, "check_py": "PASS" if res["passed"] else "FAIL",
+            "max_av_vels_pct": round(abs(res["av"]["max_diff_pcnt"]), 4) if "av" in res else None,
+            "max_final_state_pct": round(abs(res["fs"]["max_diff_pcnt"]), 4) if "fs" in res else None,
+            "reynolds": r.get("reynolds")}
+
+
+def cpu_lastchance_1024() -> dict | None:
+    """The reference's own LastChance on a bounded sample of the 1024x1024
+    reference problem, single thread on this host."""
+    from oracle import oracle  # baseline only
     iters = 500
     gold = ROOT / "tests" / "golden" / "params"
+    if not oracle.REF_LASTCHANCE.exists():
+        return None
     with tempfile.TemporaryDirectory() as wd:
         pf = Path(wd) / "bench.params"
         pf.write_text(f"1024\n1024\n{iters}\n10\n0.1\n0.01\n1.85\n")
-        of = gold / "obstacles_1024x1024.dat"
-        if oracle.REF_LASTCHANCE.exists():
-            try:
-                r = oracle.run_reference(str(pf), str(of), wd)
-                secs = r["elapsed_s"]
-                return {"value": round(1024 * 1024 * iters / secs / 1e6, 2), "unit": "MLUPS", "cores": 1,
-                        "kind": "reference",
-                        "sample": f"main/LastChance.cpp (compiled -O3 -ffp-contract=off) on the 1024x1024 "
-                                  f"reference problem, first {iters} of 20000 steps, {secs:.2f} s, 1 thread"}
-            except Exception as exc:  # fall back to the restatement
-                log(f"reference CPU baseline failed: {exc}")
-        p = lio.Params.from_file(str(pf))
-        obst = lio.read_obstacles(p.nx, p.ny, str(of))
-        t = time.perf_counter()
-        oracle.run(p, obst)
-        secs = time.perf_counter() - t
-        return {"value": round(1024 * 1024 * iters / secs / 1e6, 2), "unit": "MLUPS", "cores": 1, "kind": "port",
-                "sample": f"oracle/lbm_oracle.c restatement, 1024x1024 reference problem, {iters} steps, "
-                          f"{secs:.2f} s, 1 thread"}
+        r = oracle.run_reference(str(pf), str(gold / "obstacles_1024x1024.dat"), wd)
+    secs = r["elapsed_s"]
+    return {"value": round(1024 * 1024 * iters / secs / 1e6, 2), "unit": "MLUPS", "cores": 1, "kind": "reference",
+            "sample": f"main/LastChance.cpp on the 1024x1024 reference problem, first {iters} of 20000 steps, "
+                      f"{secs:.2f} s, 1 thread"}
 
 
 def cpu_baseline_threads() -> dict:
@@ -172,14 +227,14 @@ def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
             "reynolds": lio.reynolds_number(p, float(av[-1])), "note": note}
 
 
-def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on: bool) -> dict:
+def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on: bool, slabs: bool = False) -> dict:
     """BASELINE config 4: the fixed 16384x16384 grid (synthetic obstacles) over all
     ranks, RCCL halos overlapped with the interior -- whole-job MLUPS (strong
-    scaling; the target is >= 6x at 8 GPUs over 1).  Split into y slabs (N x 1)
-    rather than the reference's partitionForIpus blocks (1x2, 2x2, 2x4, the
-    engine's default and lbm_partition's answer): emulated on one GPU, 2/4/8
-    slabs ran 250/246/202 GLUPS against 200/199/182 for the blocks
-    (profiles/r01/stream/ab_parts_strong.log)."""
+    scaling; the target is >= 6x at 8 GPUs over 1).  Decomposition: the
+    reference's partitionForIpus rule (1x2, 2x2, 2x4: lbm_partition, the
+    engine's default), or N x 1 y slabs (slabs=True).  Untimed settle steps
+    (>= 0.2 s of device time, same count on every rank) precede the timed
+    steps."""
     import torch.distributed as dist
     n = 16384
     p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
@@ -188,11 +243,14 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
     if dist_on:
         box = [native.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-        kw.update(parts=world, grid=(world, 1), transport=native.TRANSPORT_RCCL, rank=rank, world=world,
-                  unique_id=box[0])
+        kw.update(parts=world, transport=native.TRANSPORT_RCCL, rank=rank, world=world, unique_id=box[0])
+        if slabs:
+            kw.update(grid=(world, 1))
     with native.Engine(p, obst, **kw) as e:
         e.init_equilibrium()
         e.run_steps(8, accelerate_first=True)
+        nset = _agree_max(settle_steps(e.last_run_seconds() / 8, e.steps_per_launch(), 0.2), dist_on)
+        e.run_steps(nset)
         if dist_on:
             dist.barrier()
         t0 = time.perf_counter()
@@ -207,9 +265,22 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
         t = torch.tensor([secs], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         secs = float(t[0])
-    return {"grid": f"{n}x{n}", "steps": steps, "decomposition": f"{world}x1 (y slabs)",
+    R, C, _ = native.partition(n, n, world, *((world, 1) if slabs else (0, 0)))
+    return {"grid": f"{n}x{n}", "steps": steps, "settle_steps": nset,
+            "decomposition": f"{R}x{C}" + (" (y slabs)" if slabs else " (reference partitionForIpus rule)"),
             "sub_domain": f"{rect[2]}x{rect[3]}", "kernel": kernel_used,
             "mlups": round(n * n * steps / secs / 1e6, 1), "ms_per_step": round(secs / steps * 1e3, 4)}
+
+
+def _agree_max(v: int, dist_on: bool) -> int:
+    """The largest of every rank's value (so all ranks run the same step counts)."""
+    if not dist_on:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t[0])
 
 
 def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_on: bool) -> dict:
@@ -257,11 +328,72 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
                     "that basis); parity unpinned upstream (no 3-D reference)"}
 
 
+def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: int, rank: int, world: int,
+                 local_rank: int, dist_on: bool) -> dict:
+    """K timed steps of the weak-scaling workload: R x C tiles of tnx x tny cells,
+    one per rank (R*C == world), after W warm-up and the settle steps."""
+    import torch
+    import torch.distributed as dist
+    nx, ny = tnx * C, tny * R
+    p = lio.Params(nx, ny, args.steps, 10, 0.1, 0.005, 1.85)
+    obst = synthetic_obstacles(nx, ny)
+    uid = None
+    if dist_on:
+        box = [native.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    eng = native.Engine(p, obst, parts=world, grid=(R, C),
+                        transport=native.TRANSPORT_RCCL if dist_on else native.TRANSPORT_LOCAL,
+                        rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel, flags=kflags,
+                        steps_per_launch=args.spl)
+    try:
+        eng.init_equilibrium()
+        spl = eng.steps_per_launch()
+        if args.warmup > 0:
+            eng.run_steps(args.warmup, accelerate_first=True)
+            per_step = eng.last_run_seconds() / args.warmup
+        else:
+            eng.run_steps(spl, accelerate_first=True)
+            per_step = eng.last_run_seconds() / spl
+        nset = _agree_max(settle_steps(per_step, spl, args.settle) if args.settle > 0 else 0, dist_on)
+        set_secs = 0.0
+        if nset > 0:
+            eng.run_steps(nset)
+            set_secs = eng.last_run_seconds()
+
+        def barrier():
+            if dist_on:
+                dist.barrier()
+
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.run_steps(args.steps, accelerate_first=False)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        dev_secs = eng.last_run_seconds()
+        if dist_on:
+            t = torch.tensor([elapsed, dev_secs], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, dev_secs = float(t[0]), float(t[1])
+        _, av = eng.store(cells=False, n_av=args.steps)
+        return {"nx": nx, "ny": ny, "elapsed": elapsed, "dev_secs": dev_secs, "finite": bool(np.all(np.isfinite(av))),
+                "kernel": eng.kernel_in_use(), "spl": eng.steps_per_launch(),
+                "settle": {"steps": nset, "device_s": round(set_secs, 4),
+                           "why": "GPU clock ramp over the first ~20-30 ms of back-to-back work "
+                                  "(tools/settle_probe.py); untimed, same count on every rank"}}
+    finally:
+        eng.close()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle", type=float, default=0.3,
+                    help="untimed settle steps worth this many seconds of device time after the warm-up (0: none)")
     ap.add_argument("--tile", default="8192x8192", help="cells per GPU, NXxNY")
     ap.add_argument("--kernel", default="auto", choices=["auto", "resident", "stream", "step2", "vec4", "scalar", "pipeline"],
                     help="stream: fused S-step register-streaming kernel; step2: fused two-step LDS kernel; "
@@ -280,7 +412,8 @@ def main() -> int:
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     n = world
-    kernel = {"auto": native.KERNEL_AUTO, "resident": native.KERNEL_RESIDENT, "pipeline": native.KERNEL_PIPELINE, "stream": native.KERNEL_STREAM, "step2": native.KERNEL_STEP2,
+    kernel = {"auto": native.KERNEL_AUTO, "resident": native.KERNEL_RESIDENT, "pipeline": native.KERNEL_PIPELINE,
+              "stream": native.KERNEL_STREAM, "step2": native.KERNEL_STEP2,
               "scalar": native.KERNEL_SCALAR, "vec4": native.KERNEL_VEC4}[args.kernel]
     kflags = native.FLAG_ONE_STEP if args.kernel in ("vec4", "scalar") else 0
 
@@ -293,45 +426,10 @@ def main() -> int:
     torch.cuda.set_device(local_rank)
 
     tnx, tny = (int(v) for v in args.tile.lower().split("x"))
-    R, C = weak_grid(n)
-    nx, ny = tnx * C, tny * R
-    p = lio.Params(nx, ny, args.steps, 10, 0.1, 0.005, 1.85)
-    obst = synthetic_obstacles(nx, ny)
-
-    uid = None
-    if dist_on:
-        box = [native.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
-    eng = native.Engine(p, obst, parts=n, grid=(R, C),
-                        transport=native.TRANSPORT_RCCL if dist_on else native.TRANSPORT_LOCAL,
-                        rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel, flags=kflags,
-                        steps_per_launch=args.spl)
-    eng.init_equilibrium()
-    if args.warmup > 0:
-        eng.run_steps(args.warmup, accelerate_first=True)
-
-    def barrier():
-        if dist_on:
-            dist.barrier()
-
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.run_steps(args.steps, accelerate_first=False)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    dev_secs = eng.last_run_seconds()
-    if dist_on:
-        t = torch.tensor([elapsed, dev_secs], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, dev_secs = float(t[0]), float(t[1])
-    _, av = eng.store(cells=False, n_av=args.steps)
-    finite = bool(np.all(np.isfinite(av)))
-    kernel_used = eng.kernel_in_use()
-    steps_per_launch = eng.steps_per_launch()
-    eng.close()
+    R, C = weak_grid(n, tnx, tny)
+    m = measure_weak(tnx, tny, R, C, args, kernel, kflags, rank, world, local_rank, dist_on)
+    nx, ny, elapsed, dev_secs = m["nx"], m["ny"], m["elapsed"], m["dev_secs"]
+    kernel_used, steps_per_launch = m["kernel"], m["spl"]
 
     total_cells = nx * ny
     value = total_cells * args.steps / elapsed / 1e6
@@ -360,8 +458,10 @@ def main() -> int:
         "data": "synthetic (deterministic obstacles: border walls + interior column at x=nx/3; equilibrium start)",
         "config": {"workload": f"D2Q9-BGK fused step, {tnx}x{tny} fp32 cells per GPU",
                    "global_grid": f"{nx}x{ny}", "decomposition": f"{R}x{C}",
-                   "parallelism": f"{n} y slabs, one per GPU, RCCL halo exchange" if n > 1 else "single GPU",
+                   "parallelism": (f"{R}x{C} blocks (reference partitionForIpus rule), one per GPU, RCCL halo "
+                                   f"exchange overlapped with the interior" if n > 1 else "single GPU"),
                    "kernel": kernel_used},
+        "settle": m["settle"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": BYTES_PER_UPDATE * cells_per_gpu,
@@ -372,36 +472,51 @@ def main() -> int:
                      # the lattice through HBM once per S updates, so this can exceed the peak
                      "effective_gbs": round(effective, 1),
                      "effective_frac": round(effective / HBM_PEAK_GBS, 4)},
-        "av_vels_finite": finite,
+        "av_vels_finite": m["finite"],
     }
-    if not args.no_aux and not args.no_strong:
+    aux = out.setdefault("aux", {})
+    if n > 1 and not args.no_aux:
         try:
-            aux4 = aux_strong_16384(100, rank, world, local_rank, dist_on)
+            ms = measure_weak(tnx, tny, n, 1, args, kernel, kflags, rank, world, local_rank, dist_on)
+            aux["weak_slabs"] = {"decomposition": f"{n}x1 (y slabs)", "global_grid": f"{ms['nx']}x{ms['ny']}",
+                                 "mlups": round(ms["nx"] * ms["ny"] * args.steps / ms["elapsed"] / 1e6, 1),
+                                 "ms_per_step": round(ms["elapsed"] / args.steps * 1e3, 5), "kernel": ms["kernel"]}
         except Exception as exc:
-            aux4 = {"error": str(exc)}
-        out.setdefault("aux", {})["config4_16384x16384"] = aux4
+            aux["weak_slabs"] = {"error": str(exc)}
+    if not args.no_aux and not args.no_strong:
+        for key, slabs in (("config4_16384x16384", False), ("config4_slabs", True)):
+            if slabs and n == 1:
+                continue
+            try:
+                aux[key] = aux_strong_16384(100, rank, world, local_rank, dist_on, slabs=slabs)
+            except Exception as exc:
+                aux[key] = {"error": str(exc)}
     if not args.no_aux and not args.no_d3q19:
         try:
-            aux3 = aux_d3q19(args.d3q19_n, 20, rank, world, local_rank, dist_on)
+            aux["config5_d3q19"] = aux_d3q19(args.d3q19_n, 20, rank, world, local_rank, dist_on)
         except Exception as exc:
-            aux3 = {"error": str(exc)}
-        out.setdefault("aux", {})["config5_d3q19"] = aux3
+            aux["config5_d3q19"] = {"error": str(exc)}
     if rank == 0 and n == 1:
         if not args.no_aux:
             try:
-                out.setdefault("aux", {})["config2_1024x1024"] = aux_1024(kernel, kflags, args.spl)
+                aux["config2_1024x1024"] = aux_1024(kernel, kflags, args.spl)
             except Exception as exc:
-                out.setdefault("aux", {})["config2_1024x1024"] = {"error": str(exc)}
+                aux["config2_1024x1024"] = {"error": str(exc)}
         if not args.no_cpu_baseline:
-            try:
-                out["cpu_baseline"] = cpu_baseline()
-            except Exception as exc:
-                out["cpu_baseline"] = None
-                log(f"cpu baseline failed: {exc}")
-            try:
-                out.setdefault("aux", {})["cpu_baseline_threads"] = cpu_baseline_threads()
-            except Exception as exc:
-                log(f"threaded cpu baseline failed: {exc}")
+            for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_config1_128x128", cpu_config1),
+                            ("cpu_lastchance_1024x1024", cpu_lastchance_1024),
+                            ("cpu_baseline_threads", cpu_baseline_threads)):
+                try:
+                    r = fn()
+                except Exception as exc:
+                    r = None
+                    log(f"{key} failed: {exc}")
+                if key == "cpu_baseline":
+                    out["cpu_baseline"] = r if r is not None else cpu_lastchance_1024()
+                elif r is not None:
+                    aux[key] = r
+    if not aux:
+        out.pop("aux")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist_on:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LBM_ABI_VERSION 2
+#define LBM_ABI_VERSION 3
 
 enum {
     LBM_OK = 0,
@@ -197,6 +197,22 @@ int lbm_run_steps(lbm_handle *h, int32_t steps, int32_t accelerate_first);
  * sum over ALL ranks of |u| / total free cells (may be NULL).
  */
 int lbm_store(lbm_handle *h, float *cells_aos, float *av_vels, int32_t n_av);
+
+/*
+ * Per-rank host I/O (one process per GPU at scale: a 16384^2 lattice is
+ * 9.66 GB of AoS per copy, so ranks should not each hold the full domain).
+ * cells_aos_local: this handle's local sub-domains only, each AoS
+ * float[h][w][9] of its lbm_local_rects rectangle, packed one after another
+ * in lbm_local_rects order (RCCL: the rank's one rectangle);
+ * lbm_local_cells() = the sum of w*h.  Same semantics as lbm_load_cells /
+ * lbm_store otherwise (av_vels are still the all-rank values).  A rank-0
+ * reader scatters the rectangles (lbm_amd.io.scatter_subdomains) and gathers
+ * them back for the .dat writers (gather_subdomains); the reference's
+ * single-process LbmRunner (LbmRunner.cpp:67-108) keeps using lbm_load_cells.
+ */
+int lbm_load_cells_local(lbm_handle *h, const float *cells_aos_local);
+int lbm_store_local(lbm_handle *h, float *cells_aos_local, float *av_vels, int32_t n_av);
+int64_t lbm_local_cells(lbm_handle *h);
 
 /* ≙ engine.readTensor("readTimer") (LbmRunner.cpp:133-144):
  * device-event seconds of the last lbm_run / lbm_run_steps. */

@@ -660,7 +660,7 @@ struct lbm_handle {
     // band's rows; the last tier takes the rest), "0" = uniform heights.
     template <class MK>
     bool guided_rects(int x0, int y0, int w, int h, MK &&mk, std::vector<SRect> &out) const {
-        if (stream_hs > 0 || stream_v < 2 || guide.empty()) return false;
+        if (stream_hs > 0 || stream_v != 3 || guide.empty()) return false;
         constexpr int NB = 8;
         const int hb = h / NB;
         if (hb < 2 * guide[0].first) return false;
@@ -1481,15 +1481,28 @@ struct lbm_handle {
         loaded = true;
     }
 
-    void load_cells(const float *aos) {
+    // Host AoS source / destination of sub-domain k: the full-domain array
+    // (row stride nx cells, the sub-domain at its global rectangle) or, for
+    // the *_local calls, the local sub-domains packed one after another in
+    // lbm_local_rects order (row stride w cells).
+    const float *aos_of(const float *aos, size_t k, bool local) const {
+        if (!local) return aos + ((size_t)subs[k].rect.y0 * p.nx + subs[k].rect.x0) * Q;
+        size_t off = 0;
+        for (size_t i = 0; i < k; ++i) off += (size_t)subs[i].w * subs[i].h * Q;
+        return aos + off;
+    }
+    size_t aos_pitch(const Sub &s, bool local) const { return sizeof(float) * Q * (size_t)(local ? s.w : p.nx); }
+
+    void load_cells(const float *aos, bool local = false) {
         if (!aos) throw lbm_failure(LBM_E_INVALID, "cells must not be NULL");
-        for (auto &s : subs) {
+        for (size_t k = 0; k < subs.size(); ++k) {
+            Sub &s = subs[k];
             set_device(s);
             float *stage = nullptr;
             const size_t row_bytes = sizeof(float) * Q * (size_t)s.w;
             HIP_CHECK(hipMalloc(&stage, row_bytes * (size_t)s.h));
-            HIP_CHECK(hipMemcpy2D(stage, row_bytes, aos + ((size_t)s.rect.y0 * p.nx + s.rect.x0) * Q,
-                                  sizeof(float) * Q * (size_t)p.nx, row_bytes, (size_t)s.h, hipMemcpyHostToDevice));
+            HIP_CHECK(hipMemcpy2D(stage, row_bytes, aos_of(aos, k, local), aos_pitch(s, local), row_bytes, (size_t)s.h,
+                                  hipMemcpyHostToDevice));
             s.cur = 0;
             HIP_CHECK(launch_aos_to_soa(stage, s.o[0], s.plane, s.pitch, s.w, s.h, s.s_comp));
             HIP_CHECK(hipStreamSynchronize(s.s_comp));
@@ -1500,19 +1513,20 @@ struct lbm_handle {
         loaded = true;
     }
 
-    void store(float *aos, float *av, int n_av) {
+    void store(float *aos, float *av, int n_av, bool local = false) {
         if (!loaded) throw lbm_failure(LBM_E_STATE, "nothing to store");
         sync_all();
         if (aos) {
-            for (auto &s : subs) {
+            for (size_t k = 0; k < subs.size(); ++k) {
+                Sub &s = subs[k];
                 set_device(s);
                 float *stage = nullptr;
                 const size_t row_bytes = sizeof(float) * Q * (size_t)s.w;
                 HIP_CHECK(hipMalloc(&stage, row_bytes * (size_t)s.h));
                 HIP_CHECK(launch_soa_to_aos(s.o[s.cur], stage, s.plane, s.pitch, s.w, s.h, s.s_comp));
                 HIP_CHECK(hipStreamSynchronize(s.s_comp));
-                HIP_CHECK(hipMemcpy2D(aos + ((size_t)s.rect.y0 * p.nx + s.rect.x0) * Q, sizeof(float) * Q * (size_t)p.nx,
-                                      stage, row_bytes, row_bytes, (size_t)s.h, hipMemcpyDeviceToHost));
+                HIP_CHECK(hipMemcpy2D(const_cast<float *>(aos_of(aos, k, local)), aos_pitch(s, local), stage, row_bytes,
+                                      row_bytes, (size_t)s.h, hipMemcpyDeviceToHost));
                 HIP_CHECK(hipFree(stage));
             }
         }
@@ -1705,6 +1719,23 @@ int lbm_run_steps(lbm_handle *h, int32_t steps, int32_t accelerate_first) {
 int lbm_store(lbm_handle *h, float *cells_aos, float *av_vels, int32_t n_av) {
     if (!h) return LBM_E_INVALID;
     return guarded(h, [&] { h->store(cells_aos, av_vels, n_av); });
+}
+
+int lbm_load_cells_local(lbm_handle *h, const float *cells_aos_local) {
+    if (!h) return LBM_E_INVALID;
+    return guarded(h, [&] { h->load_cells(cells_aos_local, true); });
+}
+
+int lbm_store_local(lbm_handle *h, float *cells_aos_local, float *av_vels, int32_t n_av) {
+    if (!h) return LBM_E_INVALID;
+    return guarded(h, [&] { h->store(cells_aos_local, av_vels, n_av, true); });
+}
+
+int64_t lbm_local_cells(lbm_handle *h) {
+    if (!h) return -1;
+    int64_t n = 0;
+    for (const auto &s : h->subs) n += (int64_t)s.w * s.h;
+    return n;
 }
 
 int lbm_last_run_seconds(lbm_handle *h, double *seconds) {

@@ -158,3 +158,51 @@ def write_results(filename: str, p: Params, obstacles: np.ndarray, cells: np.nda
         return True
     except OSError:
         return False
+
+
+# ---- one process per GPU: rank-0 scatter / gather of sub-domain AoS blocks ----
+#
+# With lbm_load_cells_local / lbm_store_local (include/lbm_hip.h) a rank only
+# holds its own rectangle of the lattice (16384^2 is 9.66 GB of AoS per full
+# copy).  Rank 0 keeps the full-domain array the reference's loaders and .dat
+# writers use (LbmRunner.cpp:67-113) and moves the blocks over a
+# torch.distributed process group (gloo: host tensors).
+
+def scatter_subdomains(full, rects, group=None):
+    """Rank 0: full AoS float32[ny][nx][9]; every rank: returns its block
+    full[y0:y0+h, x0:x0+w] (rects[rank], e.g. from lbm_partition)."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    x0, y0, w, h = rects[rank]
+    if rank == 0:
+        for r, (rx, ry, rw, rh) in enumerate(rects):
+            if r == 0:
+                continue
+            blk = np.ascontiguousarray(full[ry:ry + rh, rx:rx + rw], dtype=np.float32)
+            dist.send(torch.from_numpy(blk), dst=r, group=group)
+        return np.ascontiguousarray(full[y0:y0 + h, x0:x0 + w], dtype=np.float32)
+    buf = torch.empty((h, w, 9), dtype=torch.float32)
+    dist.recv(buf, src=0, group=group)
+    return buf.numpy()
+
+
+def gather_subdomains(block, rects, nx, ny, group=None):
+    """Every rank passes its block (rects[rank]); rank 0 returns the full AoS
+    float32[ny][nx][9], the others None."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    if rank != 0:
+        dist.send(torch.from_numpy(np.ascontiguousarray(block, dtype=np.float32)), dst=0, group=group)
+        return None
+    full = np.empty((ny, nx, 9), np.float32)
+    x0, y0, w, h = rects[0]
+    full[y0:y0 + h, x0:x0 + w] = block
+    for r, (rx, ry, rw, rh) in enumerate(rects):
+        if r == 0:
+            continue
+        buf = torch.empty((rh, rw, 9), dtype=torch.float32)
+        dist.recv(buf, src=r, group=group)
+        full[ry:ry + rh, rx:rx + rw] = buf.numpy()
+    return full

@@ -19,7 +19,7 @@ PKG_ROOT = Path(__file__).resolve().parent.parent          # lbm-graphcore_amd/
 LIB_PATH = Path(os.environ.get("LBM_HIP_LIB", PKG_ROOT / "build" / "liblbm_hip.so"))
 
 Q = 9
-ABI_VERSION = 2          # LBM_ABI_VERSION in include/lbm_hip.h
+ABI_VERSION = 3          # LBM_ABI_VERSION in include/lbm_hip.h
 
 LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
@@ -31,7 +31,8 @@ FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP = 1, 2
 EXPORTED = [
     "lbm_abi_version", "lbm_partition", "lbm_halo_plan", "lbm_device_count", "lbm_rccl_unique_id",
     "lbm_create", "lbm_create_ex", "lbm_load_cells", "lbm_init_equilibrium",
-    "lbm_run", "lbm_run_steps", "lbm_store", "lbm_last_run_seconds",
+    "lbm_run", "lbm_run_steps", "lbm_store", "lbm_load_cells_local", "lbm_store_local", "lbm_local_cells",
+    "lbm_last_run_seconds",
     "lbm_total_free_cells", "lbm_local_rects", "lbm_kernel_in_use", "lbm_steps_per_launch",
     "lbm_last_error", "lbm_destroy",
 ]
@@ -121,6 +122,9 @@ def load_library() -> ctypes.CDLL:
         "lbm_run": ([H], ctypes.c_int),
         "lbm_run_steps": ([H, i32, i32], ctypes.c_int),
         "lbm_store": ([H, f32p, f32p, i32], ctypes.c_int),
+        "lbm_load_cells_local": ([H, f32p], ctypes.c_int),
+        "lbm_store_local": ([H, f32p, f32p, i32], ctypes.c_int),
+        "lbm_local_cells": ([H], i64),
         "lbm_last_run_seconds": ([H, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "lbm_total_free_cells": ([H], i64),
         "lbm_local_rects": ([H, ctypes.POINTER(Rect), i32, i32p], ctypes.c_int),
@@ -249,6 +253,34 @@ class Engine:
         out = np.zeros((self.params.ny, self.params.nx, Q), np.float32) if cells else None
         av = np.zeros(max(n_av, 1), np.float32)
         self._check(self._L.lbm_store(self._h, _f32(out) if cells else None, _f32(av), n_av))
+        return out, av[:n_av]
+
+    def load_cells_local(self, blocks) -> None:
+        """This handle's sub-domains only: one AoS float32[h][w][9] per local rect
+        (local_rects() order), as lbm_load_cells_local takes them packed."""
+        rects = self.local_rects()
+        if len(blocks) != len(rects):
+            raise ValueError("one block per local rect")
+        for b, (_, _, w, h) in zip(blocks, rects):
+            if tuple(np.shape(b)) != (h, w, Q):
+                raise ValueError(f"block shape {np.shape(b)} != {(h, w, Q)}")
+        packed = np.ascontiguousarray(np.concatenate([np.asarray(b, np.float32).reshape(-1) for b in blocks]))
+        assert packed.size == int(self._L.lbm_local_cells(self._h)) * Q
+        self._check(self._L.lbm_load_cells_local(self._h, _f32(packed)))
+
+    def store_local(self, cells: bool = True, n_av: int | None = None):
+        """Returns ([AoS float32[h][w][9] per local rect] or None, av_vels float32[n_av])."""
+        n_av = int(self.params.max_iters if n_av is None else n_av)
+        rects = self.local_rects()
+        packed = np.zeros(int(self._L.lbm_local_cells(self._h)) * Q, np.float32) if cells else None
+        av = np.zeros(max(n_av, 1), np.float32)
+        self._check(self._L.lbm_store_local(self._h, _f32(packed) if cells else None, _f32(av), n_av))
+        if not cells:
+            return None, av[:n_av]
+        out, off = [], 0
+        for (_, _, w, h) in rects:
+            out.append(packed[off:off + w * h * Q].reshape(h, w, Q))
+            off += w * h * Q
         return out, av[:n_av]
 
     def last_run_seconds(self) -> float:

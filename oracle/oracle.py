@@ -259,3 +259,39 @@ def run_reference(params_file: str, obstacles_file: str, workdir: str | None = N
         if line.startswith("Reynolds number:"):
             out["reynolds"] = float(line.split()[2])
     return out
+
+
+def run_lbm_cpu(params_file: str, obstacles_file: str, workdir: str | None = None,
+                binary: Path = REF_LBMCPU) -> dict:
+    """Run the reference's main/LbmCpu.cpp as committed (oracle/_ref/lbm_cpu) --
+    a cost-only baseline: its live kernel is numerically broken upstream
+    (SURVEY.md 8c), so its outputs are not checked.  Its timed region
+    (LbmCpu.cpp:404-419) includes a full-lattice printf, sent to a file here.
+    Returns {"compute_s": the program's own "Total compute time", ...}."""
+    if not binary.exists():
+        raise FileNotFoundError(f"{binary} not built (needs /root/reference at build time)")
+    wd = workdir or tempfile.mkdtemp(prefix="lbm_cpu_")
+    with open(os.path.join(wd, "stdout.txt"), "w") as so:
+        proc = subprocess.run([str(binary), "--params", os.path.abspath(params_file),
+                               "--obstacles", os.path.abspath(obstacles_file)],
+                              cwd=wd, stdout=so, stderr=subprocess.PIPE, text=True, check=True)
+    out = {"workdir": wd, "stderr": proc.stderr}
+    with open(os.path.join(wd, "stdout.txt")) as f:
+        for line in f:
+            if line.startswith("Total compute time was"):
+                out["compute_s"] = float(line.split()[-1].rstrip("s"))
+    return out
+
+
+def cpu_model() -> str:
+    """Host CPU model name (/proc/cpuinfo) and logical CPU count."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{name} ({os.cpu_count()} logical CPUs visible)"

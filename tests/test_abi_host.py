@@ -50,7 +50,7 @@ def test_library_exports_every_declared_symbol():
                          check=True).stdout
     for s in syms:
         assert re.search(rf"\bT {s}\b", out), s
-    assert L.lbm_abi_version() == 2
+    assert L.lbm_abi_version() == 3
 
 
 def test_no_torch_types_in_abi():

@@ -500,3 +500,103 @@ def test_pipeline_reference_grid_full_run(gpu_lib, grid, tmp_path):
     d = lcheck.diff_values(lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz"),
                            lcheck.load_av_vels(tmp_path / "av_vels.dat"))
     assert abs(d["max_diff_pcnt"]) < 1.0
+
+
+# ------------------------------------- wide decomposed x bands (stream) ----
+
+@pytest.mark.parametrize("nx", [1030, 1031])
+@pytest.mark.parametrize("version", [1, 2, 3])
+@pytest.mark.parametrize("S", [2, 3, 4])
+def test_stream_wide_x_bands_bitwise(gpu_lib, nx, version, S, monkeypatch):
+    """Sub-domains wide enough (>= 4 strips) for the strip-wide x boundary band
+    of a decomposed x side (lbm_engine.hip stream_split: xb = one strip, the
+    right band's owned width depending on its first column's parity, the
+    interior starting at x0 = xb): 1x2 and 2x2 loop-back with widths 515/516,
+    an odd total width, a one-step remainder, and the forced-exchange variant
+    (every wrap through the transport) -- bitwise vs the oracle."""
+    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    ny = 40
+    p = lio.Params(nx, ny, 9, 10, 0.1, 0.02, 1.7)
+    rng = np.random.default_rng(nx + 10 * S + version)
+    obst = (rng.random((ny, nx)) < 0.03).astype(np.uint8)
+    obst[:, 500:503] = 1  # a wall across the band seam region
+    cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((ny, nx, 9)))).astype(np.float32)
+    steps = 2 * S + 1
+    ref, ref_av = oracle.run(p, obst, steps, cells0)
+    for kw in (dict(parts=2, grid=(1, 2)), dict(parts=4, grid=(2, 2)),
+               dict(parts=2, grid=(1, 2), flags=gpu_lib.FLAG_FORCE_EXCHANGE)):
+        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, steps, devices=[0], kernel=gpu_lib.KERNEL_STREAM,
+                                  steps_per_launch=S, **kw)
+        assert used == "stream"
+        assert np.array_equal(cells, ref), kw
+        np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+# ------------------------------- packed division on adversarial states ----
+
+def _adversarial_state(nx, ny, seed):
+    """Rows of equilibrium-like cells whose density spans binades 2^-126..2^40
+    (row-wise scale), with perturbations so the momentum numerators are exactly
+    zero (unperturbed rows), tiny normal, or subnormal (the smallest scales)."""
+    rng = np.random.default_rng(seed)
+    scales = 2.0 ** np.array([0, -20, -60, -100, -110, -118, -122, -124, -126, 20, 40], dtype=np.float64)
+    w = np.array([4 / 9] + [1 / 9] * 4 + [1 / 36] * 4, np.float64)
+    cells = np.empty((ny, nx, 9), np.float64)
+    for y in range(ny):
+        sc = scales[y % len(scales)]
+        base = 0.1 * sc * w
+        pert = 1 + (0 if y % 3 == 0 else 1e-3 * rng.standard_normal((nx, 9)))
+        cells[y] = base * pert
+    return cells.astype(np.float32)
+
+
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "resident", "vec4", "step2"])
+@pytest.mark.parametrize("version", [2, 3])
+def test_division_adversarial_states_bitwise(gpu_lib, mode, version, monkeypatch):
+    """lbm_packed.hpp's short division sequences (x/9, x/36 by multiply + two
+    corrections; n/rho without v_div_scale / v_div_fixup) against the oracle's
+    correctly rounded '/' on states where the momentum numerators are zero,
+    tiny normal or subnormal and rho spans many binades (down to the smallest
+    normals): the lattice must stay bitwise equal.  One step and three steps,
+    no obstacles and no acceleration (so the states stay in their binades)."""
+    if version == 3 and not mode.startswith("stream"):
+        pytest.skip("LBM_STREAM_V only selects the stream kernel")
+    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    monkeypatch.setenv("LBM_RES_V", "2")  # the packed resident kernel (collide2)
+    nx, ny = 256, 66
+    p = lio.Params(nx, ny, 3, 10, 0.1, 0.0, 1.85)
+    obst = np.zeros((ny, nx), np.uint8)
+    cells0 = _adversarial_state(nx, ny, 5)
+    for steps in (1, 3):
+        ref, _ = oracle.run(p, obst, steps, cells0)
+        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, steps, **mode_kw(gpu_lib, mode))
+        assert used == kname(mode)
+        same = cells.view(np.uint32) == ref.view(np.uint32)
+        if not same.all():
+            bad = np.argwhere(~same)
+            y, x, k = bad[0]
+            pytest.fail(f"{mode} v{version} {steps} steps: {len(bad)} values differ, first at y={y} x={x} k={k}: "
+                        f"gpu {cells[y, x, k]!r} oracle {ref[y, x, k]!r}")
+
+
+# ------------------------------------------------ per-rank local I/O ----
+
+@pytest.mark.parametrize("parts,grid", [(1, (1, 1)), (4, (2, 2)), (3, (1, 3))])
+def test_local_load_store_matches_full(gpu_lib, parts, grid):
+    """lbm_load_cells_local / lbm_store_local (each sub-domain's own AoS block,
+    local_rects order) give the same run as the full-domain load / store."""
+    p, obst = load_problem("128x256", iters=10)
+    rng = np.random.default_rng(3)
+    cells0 = (lio.init_cells(p) * (1 + 0.02 * rng.standard_normal((p.ny, p.nx, 9)))).astype(np.float32)
+    ref, ref_av = oracle.run(p, obst, 10, cells0)
+    with gpu_lib.Engine(p, obst, parts=parts, grid=grid, devices=[0]) as e:
+        rects = e.local_rects()
+        e.load_cells_local([cells0[y0:y0 + h, x0:x0 + w] for (x0, y0, w, h) in rects])
+        e.run_steps(10, accelerate_first=True)
+        blocks, av = e.store_local(n_av=10)
+        full, av_full = e.store(n_av=10)
+    assert np.array_equal(full, ref)
+    for (x0, y0, w, h), b in zip(rects, blocks):
+        assert np.array_equal(b, ref[y0:y0 + h, x0:x0 + w])
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+    assert np.array_equal(av, av_full)
