@@ -177,29 +177,28 @@ __device__ __forceinline__ float cell3d(const float (&s)[Q3], float (&o)[Q3], bo
     }
     const float rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8] + s[9] + s[10] + s[11] + s[12] +
                       s[13] + s[14] + s[15] + s[16] + s[17] + s[18];
-    // the correctly rounded divisions by exact short sequences (lbm_packed.hpp
-    // header; tools/check_fastdiv.c: every x for d = 3, 18, 36, and n / rho):
-    // one reciprocal refinement shared by the three velocity components
-    const float nrho = -rho;
-    const float r0 = __builtin_amdgcn_rcpf(rho);
-    const float rr = __builtin_fmaf(__builtin_fmaf(nrho, r0, 1.0f), r0, r0);
-    auto qdiv = [&](float n) {
-        float q = n * rr;
-        q = __builtin_fmaf(__builtin_fmaf(nrho, q, n), rr, q);
-        return __builtin_fmaf(__builtin_fmaf(nrho, q, n), rr, q);
-    };
+    // correctly rounded divisions for every input (lbm_packed.hpp header):
+    // the velocity components by the compiler's IEEE sequence; x/3 by the
+    // short sequence (exhaustively exact for every float x); x/18 and x/36
+    // by it for x >= 2^-120 (exhaustive: exact from 2^-125 / 2^-124 up), by
+    // IEEE division in a wave holding a smaller density (never in physical states)
     auto cdiv = [](float x, float d, float y) {
         const float q = x * y;
         return __builtin_fmaf(__builtin_fmaf(-d, q, x), y, q);
     };
-    const float ux = qdiv((s[1] + s[5] + s[7] + s[10] + s[16]) - (s[2] + s[6] + s[8] + s[11] + s[15]));
-    const float uy = qdiv((s[3] + s[5] + s[8] + s[12] + s[18]) - (s[4] + s[6] + s[7] + s[13] + s[17]));
-    const float uz = qdiv((s[9] + s[10] + s[11] + s[12] + s[13]) - (s[14] + s[15] + s[16] + s[17] + s[18]));
+    const float ux = ((s[1] + s[5] + s[7] + s[10] + s[16]) - (s[2] + s[6] + s[8] + s[11] + s[15])) / rho;
+    const float uy = ((s[3] + s[5] + s[8] + s[12] + s[18]) - (s[4] + s[6] + s[7] + s[13] + s[17])) / rho;
+    const float uz = ((s[9] + s[10] + s[11] + s[12] + s[13]) - (s[14] + s[15] + s[16] + s[17] + s[18])) / rho;
     const float usq = ux * ux + uy * uy + uz * uz;
     const float c = 1.00f - usq * 1.50f;
     const float ld0 = cdiv(rho, 3.00f, 1.00f / 3.00f) * omega;
-    const float ld1 = cdiv(rho, 18.00f, 1.00f / 18.00f) * omega;
-    const float ld2 = cdiv(rho, 36.00f, 1.00f / 36.00f) * omega;
+    float r18 = cdiv(rho, 18.00f, 1.00f / 18.00f), r36 = cdiv(rho, 36.00f, 1.00f / 36.00f);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(rho >= 0x1p-120f)) != 0, 0)) {
+        r18 = rho / 18.00f;
+        r36 = rho / 36.00f;
+    }
+    const float ld1 = r18 * omega;
+    const float ld2 = r36 * omega;
     const float pxy = ux + uy, mxy = ux - uy, pxz = ux + uz, mxz = -ux + uz, pyz = uy + uz, myz = -uy + uz;
     const float e[Q3] = {0.f, ux, -ux, uy, -uy, pxy, -pxy, mxy, -mxy, uz, pxz, mxz, pyz, myz,
                          -uz, -pxz, -mxz, -pyz, -myz};

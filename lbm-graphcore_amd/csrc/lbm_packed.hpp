@@ -5,17 +5,18 @@
 // Bitwise parity with the one-step kernels and the CPU oracle: every
 // expression is evaluated in the order of LastChance.cpp:226-262 with one
 // rounding per operation (packed ops round each lane like their scalar
-// forms; no contraction).  The two kinds of correctly rounded operations
-// use shorter exact sequences than the compiler's general expansions:
-//   * x / 9 and x / 36: q = x*y, r = fma(-d, q, x), q' = fma(r, y, q) with
-//     y = RN(1/d) -- exhaustively checked equal to RN(x/d) over 41 binades
-//     (every normal x with x/d normal behaves the same; tools/check_fastdiv.c);
-//   * n / rho: the LLVM AMDGPU IEEE division expansion (rcp, one Newton step,
-//     two residual corrections) minus its v_div_scale / v_div_fixup
-//     wrappers, which only act when an operand is within 2^64 of the
-//     exponent limits, 0, inf or NaN (densities are ~0.1 and momenta
-//     either 0 or far above 2^-100 in any physical state); the reciprocal
-//     refinement is shared by u_x and u_y;
+// forms; no contraction).  Divisions stay correctly rounded for EVERY input:
+//   * n / rho: the compiler's IEEE sequence (v_div_scale, v_rcp, four fma,
+//     v_div_fmas, v_div_fixup).  A shorter sequence without the scale / fixup
+//     wrappers (round 1) is exact only while rho, n and n/rho stay clear of
+//     the exponent limits (tools/check_fastdiv.c --probe); on states with
+//     tiny densities it produced NaN where the oracle did not
+//     (tests/test_gpu_parity.py test_division_adversarial_states_bitwise);
+//   * x / 9: q = x*y, r = fma(-9, q, x), q' = fma(r, y, q) with y = RN(1/9) --
+//     exhaustively equal to RN(x/9) for every float x;
+//   * x / 36: the same sequence is exact for x >= 2^-124 (exhaustive); a wave
+//     holding a smaller density takes the compiler's IEEE division instead
+//     (a wave-uniform branch, never taken in physical states).
 // |u| = sqrt(u^2) feeds only av_vels and uses v_sqrt_f32 (sqrt_av below).
 #pragma once
 
@@ -47,18 +48,12 @@ __device__ __forceinline__ f2 div_const(f2 x) {
     return fma2(r, mk2(y), q);
 }
 
-// RN(nx / d), RN(ny / d) sharing the reciprocal refinement (see header)
-__device__ __forceinline__ void div_pair(f2 nx, f2 ny, f2 d, f2 &qx, f2 &qy) {
-    const f2 r0 = f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    const f2 nd = -d;
-    const f2 e = fma2(nd, r0, mk2(1.0f));
-    const f2 r = fma2(e, r0, r0);
-    f2 q = nx * r;
-    q = fma2(fma2(nd, q, nx), r, q);
-    qx = fma2(fma2(nd, q, nx), r, q);
-    f2 p = ny * r;
-    p = fma2(fma2(nd, p, ny), r, p);
-    qy = fma2(fma2(nd, p, ny), r, p);
+// RN(x / 36) for every x: the short sequence unless some lane of the wave
+// holds x < 2^-120 (or a negative / NaN x), then IEEE division (see header)
+__device__ __forceinline__ f2 div36_exact(f2 x) {
+    const bool tiny = __builtin_amdgcn_ballot_w64(!(x.x >= 0x1p-120f) || !(x.y >= 0x1p-120f)) != 0;
+    if (__builtin_expect(tiny, 0)) return x / mk2(36.0f);
+    return div_const<36>(x);
 }
 
 // |u| for av_vels only (never fed back into the lattice): v_sqrt_f32, within
@@ -74,12 +69,12 @@ __device__ __forceinline__ float sqrt_av(float x) { return __builtin_amdgcn_sqrt
 __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, float accf,
                                        float omega, float omo, float w1, float w2) {
     const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
-    f2 ux, uy;
-    div_pair(s[1] + s[5] + s[8] - (s[3] + s[6] + s[7]), s[2] + s[5] + s[6] - (s[4] + s[7] + s[8]), rho, ux, uy);
+    const f2 ux = (s[1] + s[5] + s[8] - (s[3] + s[6] + s[7])) / rho;
+    const f2 uy = (s[2] + s[5] + s[6] - (s[4] + s[7] + s[8])) / rho;
     const f2 usq = ux * ux + uy * uy;
     const f2 csq = mk2(1.00f) - usq * mk2(1.50f);
     const f2 ld1 = div_const<9>(rho) * mk2(omega);
-    const f2 ld2 = div_const<36>(rho) * mk2(omega);
+    const f2 ld2 = div36_exact(rho) * mk2(omega);
     const f2 OMO = mk2(omo);
     const f2 c23 = mk2(2.00f / 3.00f);
     const f2 c45 = mk2(4.50f), n45 = mk2(-4.50f);
@@ -129,12 +124,12 @@ __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bo
 __device__ __forceinline__ f2 collide2u(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, bool accrow,
                                         float omega, float omo, float w1, float w2) {
     const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
-    f2 ux, uy;
-    div_pair(s[1] + s[5] + s[8] - (s[3] + s[6] + s[7]), s[2] + s[5] + s[6] - (s[4] + s[7] + s[8]), rho, ux, uy);
+    const f2 ux = (s[1] + s[5] + s[8] - (s[3] + s[6] + s[7])) / rho;
+    const f2 uy = (s[2] + s[5] + s[6] - (s[4] + s[7] + s[8])) / rho;
     const f2 usq = ux * ux + uy * uy;
     const f2 csq = mk2(1.00f) - usq * mk2(1.50f);
     const f2 ld1 = div_const<9>(rho) * mk2(omega);
-    const f2 ld2 = div_const<36>(rho) * mk2(omega);
+    const f2 ld2 = div36_exact(rho) * mk2(omega);
     const f2 OMO = mk2(omo);
     const f2 c23 = mk2(2.00f / 3.00f);
     const f2 c45 = mk2(4.50f), n45 = mk2(-4.50f);
