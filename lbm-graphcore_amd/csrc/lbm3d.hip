@@ -351,12 +351,13 @@ constexpr int T3LDS = (2 + 2 * 6 + 3 * 2) * T3C;  // floats per level: M, Z[2][6
 struct Two3Args {
     const float *fin;   // origin of the lattice read (ghost planes -2, -1, nz, nz + 1 filled)
     float *fout;
-    const uint8_t *obst;  // [nz][ny][nx]
+    const uint8_t *obst;  // plane 0 of [nz + 4][ny][nx]: two planes of neighbour / periodic images each side
     long long PL, KS;
     int px, nx, ny, nz, seg;
+    int z0, zn;           // output planes [z0, zn) of this launch, in segments of seg planes
     float omega, omo, w1, w2;
-    float *partials;      // [2][nblocks]: |u| of step t+1, then t+2
-    int nblocks;
+    float *partials;      // [2][nblocks]: |u| of step t+1, then t+2, at blk0 + this launch's block
+    int nblocks, blk0;
 };
 
 // One level for centre plane jz - 1, input plane jz (in).  Must be reached by
@@ -417,13 +418,13 @@ __global__ __launch_bounds__(T3W * T3H) void step3d_two(Two3Args a) {
     const int y = (((oy - 2 + wy) % a.ny) + a.ny) % a.ny;
     const bool own = lane >= 2 && lane < T3W - 2 && wy >= 2 && wy < T3H - 2 && ox + lane - 2 < a.nx &&
                      oy + wy - 2 < a.ny;
-    const int zs = blockIdx.z * a.seg, ze = min(zs + a.seg, a.nz);
+    const int zs = a.z0 + blockIdx.z * a.seg, ze = min(zs + a.seg, a.zn);
     const long long row = (long long)y * a.px + x;
     float r0a[3] = {0.f, 0.f, 0.f}, r9aa[3] = {0.f, 0.f, 0.f}, r9ba[3] = {0.f, 0.f, 0.f};
     float r0b[3] = {0.f, 0.f, 0.f}, r9ab[3] = {0.f, 0.f, 0.f}, r9bb[3] = {0.f, 0.f, 0.f};
     float u1 = 0.f, u2 = 0.f;
-    auto obz = [&](int zz) {
-        zz = ((zz % a.nz) + a.nz) % a.nz;
+    auto obz = [&](int zz) {  // planes zs-4 .. ze are asked for; only zs-1 .. ze are used
+        zz = min(max(zz, -2), a.nz + 1);
         return a.obst[((long long)zz * a.ny + y) * a.nx + x] != 0;
     };
     // input planes are prefetched one iteration ahead (their loads stay in
@@ -472,7 +473,7 @@ __global__ __launch_bounds__(T3W * T3H) void step3d_two(Two3Args a) {
             b1 += red[0][i];
             b2 += red[1][i];
         }
-        const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const int blk = a.blk0 + (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
         a.partials[blk] = b1;
         a.partials[a.nblocks + blk] = b2;
     }
@@ -550,6 +551,7 @@ struct Slab {
     float *f[2] = {nullptr, nullptr};  // allocations (ghost plane below first)
     float *o[2] = {nullptr, nullptr};  // origins: plane z = 0
     uint8_t *obst = nullptr;
+    uint8_t *obst_g = nullptr;   // [nzs + 4][ny][nx]: obst with two image planes each side (two-step kernel)
     float *partials = nullptr;
     int nblk_all = 0, nblk_bnd = 0, nblk_int = 0;
     float *partials2 = nullptr;  // two-step kernel: [2][nblk_two]
@@ -573,7 +575,7 @@ struct lbm3d_handle {
     // non-temporal stores (the lattice written now is read a whole step later)
     int zb = 2;        // LBM3D_ZB: planes per block of the pair kernel (1, 2, 4, 8)
     bool nt = true;    // LBM3D_NT: non-temporal output stores
-    bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two) on a single slab
+    bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two), single slab or z slabs
     int seg = 64;      // LBM3D_SEG: z planes per block of the two-step kernel (32-128 equal within noise at 512^3)
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
@@ -685,19 +687,23 @@ struct lbm3d_handle {
             H3(hipMemset(s.f[k], 0, floats * sizeof(float)));
             s.o[k] = s.f[k] + 2 * PL;
         }
-        const size_t ob = (size_t)s.nzs * p.ny * p.nx;
+        const size_t ob = (size_t)s.nzs * p.ny * p.nx, plane = (size_t)p.ny * p.nx;
         H3(hipMalloc(&s.obst, ob + 256));
-        H3(hipMemcpy(s.obst, obstacles + (size_t)s.z0 * p.ny * p.nx, ob, hipMemcpyHostToDevice));
+        H3(hipMemcpy(s.obst, obstacles + (size_t)s.z0 * plane, ob, hipMemcpyHostToDevice));
+        H3(hipMalloc(&s.obst_g, (size_t)(s.nzs + 4) * plane + 256));
+        for (int z = -2; z < s.nzs + 2; ++z) {  // global periodic images (the neighbour slabs' planes)
+            const int gz = ((s.z0 + z) % p.nz + p.nz) % p.nz;
+            H3(hipMemcpy(s.obst_g + (size_t)(z + 2) * plane, obstacles + (size_t)gz * plane, plane,
+                         hipMemcpyHostToDevice));
+        }
         // multi: two one-plane boundary launches, then the interior launch
         s.nblk_bnd = multi() ? (s.nzs >= 2 ? 2 : 1) * blocks_for(1) : 0;
         s.nblk_int = multi() ? blocks_for(s.nzs - 2) : 0;
         s.nblk_all = multi() ? s.nblk_bnd + s.nblk_int : blocks_for(s.nzs);
         H3(hipMalloc(&s.partials, sizeof(float) * (size_t)(s.nblk_all + 64)));
-        if (!multi()) {
-            const dim3 g = two_grid(s);
-            s.nblk_two = (int)(g.x * g.y * g.z);
-            H3(hipMalloc(&s.partials2, sizeof(float) * (2 * (size_t)s.nblk_two + 64)));
-        }
+        s.nblk_two = 0;
+        for (const auto &r : two_ranges(s)) s.nblk_two += two_blocks(r.first, r.second);
+        H3(hipMalloc(&s.partials2, sizeof(float) * (2 * (size_t)std::max(s.nblk_two, 1) + 64)));
         H3(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
         H3(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
         int lo = 0, hi = 0;
@@ -706,24 +712,35 @@ struct lbm3d_handle {
         for (hipEvent_t *e : {&s.ev_b, &s.ev_i, &s.ev_x, &s.ev_end}) H3(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
 
-    dim3 two_grid(const Slab &s) const {
-        return dim3((p.nx + T3OX - 1) / T3OX, (p.ny + T3OY - 1) / T3OY, (s.nzs + seg - 1) / seg);
+    // Output plane ranges of one two-step pass of slab s, in launch order.
+    // Single slab: all planes.  z slabs: the two boundary pairs [0, 2) and
+    // [nzs-2, nzs) first (their outputs are the next pass's exchanged ghost
+    // planes), then the interior [2, nzs-2), which reads no ghost plane and
+    // runs while the exchange moves.
+    std::vector<std::pair<int, int>> two_ranges(const Slab &s) const {
+        if (!multi() || s.nzs < 4) return {{0, s.nzs}};
+        std::vector<std::pair<int, int>> r = {{0, 2}, {s.nzs - 2, s.nzs}};
+        if (s.nzs > 4) r.push_back({2, s.nzs - 2});
+        return r;
+    }
+    int two_blocks(int z0, int zn) const {
+        return ((p.nx + T3OX - 1) / T3OX) * ((p.ny + T3OY - 1) / T3OY) * ((zn - z0 + seg - 1) / seg);
+    }
+    // two-step passes: one slab, or z slabs of at least 4 planes (ghosts are 2 planes of the neighbours)
+    bool use_two() const {
+        if (!two) return false;
+        if (!multi()) return true;
+        for (int n : all_nz)
+            if (n < 4) return false;
+        return true;
     }
 
-    // two-step pass: ghost planes -2, -1, nz, nz + 1 of the current lattice
-    // (periodic images, all 19 speeds), then step3d_two, then both steps' |u|
-    void step_two(int t) {
-        Slab &s = slabs[0];
-        const size_t bytes = sizeof(float) * (size_t)PL;
-        float *o = s.o[s.cur];
-        for (int g : {-2, -1, s.nzs, s.nzs + 1}) {
-            const int src = ((g % s.nzs) + s.nzs) % s.nzs;
-            H3(hipMemcpyAsync(o + (long long)g * PL, o + (long long)src * PL, bytes, hipMemcpyDeviceToDevice, s.s_comp));
-        }
+    void launch_two(Slab &s, int z0, int zn, int blk0, hipStream_t st) {
+        if (zn <= z0) return;
         Two3Args a{};
-        a.fin = o;
+        a.fin = s.o[s.cur];
         a.fout = s.o[1 - s.cur];
-        a.obst = s.obst;
+        a.obst = s.obst_g + (size_t)2 * p.ny * p.nx;
         a.PL = PL;
         a.KS = KS;
         a.px = px;
@@ -731,18 +748,118 @@ struct lbm3d_handle {
         a.ny = p.ny;
         a.nz = s.nzs;
         a.seg = seg;
+        a.z0 = z0;
+        a.zn = zn;
         a.omega = p.omega;
         a.omo = 1 - p.omega;
         a.w1 = w1();
         a.w2 = w2();
         a.partials = s.partials2;
         a.nblocks = s.nblk_two;
-        hipLaunchKernelGGL(step3d_two, two_grid(s), dim3(T3W, T3H), 0, s.s_comp, a);
+        a.blk0 = blk0;
+        const dim3 g((p.nx + T3OX - 1) / T3OX, (p.ny + T3OY - 1) / T3OY, (zn - z0 + seg - 1) / seg);
+        hipLaunchKernelGGL(step3d_two, g, dim3(T3W, T3H), 0, st, a);
         H3(hipGetLastError());
-        hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials2, s.nblk_two, s.av_local, t);
-        hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials2 + s.nblk_two, s.nblk_two,
-                           s.av_local, t + 1);
+    }
+
+    void reduce_two(Slab &s, int t, hipStream_t st) {
+        hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, st, s.partials2, s.nblk_two, s.av_local, t);
+        hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, st, s.partials2 + s.nblk_two, s.nblk_two, s.av_local,
+                           t + 1);
         H3(hipGetLastError());
+    }
+
+    // Two-plane ghost exchange of lattice l (all 19 speeds): planes nzs-2,
+    // nzs-1 go up into the next slab's ghosts -2, -1; planes 0, 1 go down into
+    // the previous slab's ghosts nzs, nzs+1.  Every rank posts send up, send
+    // down, recv from below, recv from above (RCCL matches by order).
+    void exchange2(int l, bool use_comm) {
+        const size_t n2 = 2 * (size_t)PL;
+        auto top = [&](const Slab &s) { return s.o[l] + (long long)(s.nzs - 2) * PL; };
+        auto bottom = [&](const Slab &s) { return s.o[l]; };
+        auto ghost_lo = [&](const Slab &s) { return s.o[l] - 2 * PL; };
+        auto ghost_hi = [&](const Slab &s) { return s.o[l] + (long long)s.nzs * PL; };
+        if (transport == LBM_TRANSPORT_RCCL) {
+            Slab &s = slabs[0];
+            H3(hipSetDevice(s.dev));
+            hipStream_t st = use_comm ? s.s_comm : s.s_comp;
+            H3(hipStreamWaitEvent(st, s.ev_b, 0));
+            const int up = (rank + 1) % world, down = (rank + world - 1) % world;
+            N3(ncclGroupStart());
+            N3(ncclSend(top(s), n2, ncclFloat, up, comm, st));
+            N3(ncclSend(bottom(s), n2, ncclFloat, down, comm, st));
+            N3(ncclRecv(ghost_lo(s), n2, ncclFloat, down, comm, st));
+            N3(ncclRecv(ghost_hi(s), n2, ncclFloat, up, comm, st));
+            N3(ncclGroupEnd());
+            H3(hipEventRecord(s.ev_x, st));
+            return;
+        }
+        for (auto &s : slabs) {  // LOCAL: each slab pulls its two ghost pairs
+            H3(hipSetDevice(s.dev));
+            hipStream_t st = use_comm ? s.s_comm : s.s_comp;
+            Slab *below = local((s.id + parts - 1) % parts), *above = local((s.id + 1) % parts);
+            H3(hipStreamWaitEvent(st, below->ev_b, 0));
+            H3(hipStreamWaitEvent(st, above->ev_b, 0));
+            const size_t bytes = sizeof(float) * n2;
+            if (below->dev == s.dev)
+                H3(hipMemcpyAsync(ghost_lo(s), top(*below), bytes, hipMemcpyDeviceToDevice, st));
+            else
+                H3(hipMemcpyPeerAsync(ghost_lo(s), s.dev, top(*below), below->dev, bytes, st));
+            if (above->dev == s.dev)
+                H3(hipMemcpyAsync(ghost_hi(s), bottom(*above), bytes, hipMemcpyDeviceToDevice, st));
+            else
+                H3(hipMemcpyPeerAsync(ghost_hi(s), s.dev, bottom(*above), above->dev, bytes, st));
+            H3(hipEventRecord(s.ev_x, st));
+        }
+    }
+
+    // Two steps of every slab (z slabs): B(t) = the boundary pairs on the
+    // high-priority stream after I(t-1) and the exchange that filled our
+    // ghosts; X(t) = their planes to the neighbours on the comm stream; I(t) =
+    // the interior on the compute stream, overlapping X(t); then both steps'
+    // |u| folds.  (Mirrors step_once's one-plane schedule.)
+    void step_two_multi(int t) {
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            H3(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
+            wait_x(s, s.s_bnd);
+            const auto r = two_ranges(s);
+            int blk = 0;
+            for (size_t i = 0; i < r.size() && i < 2; ++i) {
+                launch_two(s, r[i].first, r[i].second, blk, s.s_bnd);
+                blk += two_blocks(r[i].first, r[i].second);
+            }
+            H3(hipEventRecord(s.ev_b, s.s_bnd));
+        }
+        exchange2(1 - slabs[0].cur, true);
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            const auto r = two_ranges(s);
+            if (r.size() > 2) launch_two(s, r[2].first, r[2].second, two_blocks(r[0].first, r[0].second) +
+                                                                          two_blocks(r[1].first, r[1].second), s.s_comp);
+            H3(hipStreamWaitEvent(s.s_comp, s.ev_b, 0));
+            reduce_two(s, t, s.s_comp);
+            H3(hipEventRecord(s.ev_i, s.s_comp));
+            s.cur ^= 1;
+        }
+    }
+
+    // two-step pass: ghost planes -2, -1, nz, nz + 1 of the current lattice
+    // (periodic images, all 19 speeds), then step3d_two, then both steps' |u|
+    void step_two(int t) {
+        if (multi()) {
+            step_two_multi(t);
+            return;
+        }
+        Slab &s = slabs[0];
+        const size_t bytes = sizeof(float) * (size_t)PL;
+        float *o = s.o[s.cur];
+        for (int g : {-2, -1, s.nzs, s.nzs + 1}) {
+            const int src = ((g % s.nzs) + s.nzs) % s.nzs;
+            H3(hipMemcpyAsync(o + (long long)g * PL, o + (long long)src * PL, bytes, hipMemcpyDeviceToDevice, s.s_comp));
+        }
+        launch_two(s, 0, s.nzs, 0, s.s_comp);
+        reduce_two(s, t, s.s_comp);
         s.cur ^= 1;
         exchange(s.cur, false);  // faces for a one-step launch that may follow
     }
@@ -929,8 +1046,16 @@ struct lbm3d_handle {
             H3(hipEventRecord(s.ev_x, s.s_comp));
         }
         int t = 0;
-        if (!multi() && two)
+        if (use_two() && steps >= 2) {
+            if (multi()) {  // two-plane ghosts of the current lattice (a one-step launch leaves only its five speeds)
+                for (auto &s : slabs) {
+                    H3(hipSetDevice(s.dev));
+                    H3(hipEventRecord(s.ev_b, s.s_comp));
+                }
+                exchange2(slabs[0].cur, false);
+            }
             for (; t + 2 <= steps; t += 2) step_two(t);
+        }
         for (; t < steps; ++t) step_once(t);
         for (auto &s : slabs) {
             H3(hipSetDevice(s.dev));
@@ -1040,6 +1165,7 @@ struct lbm3d_handle {
             for (int k = 0; k < 2; ++k)
                 if (s.f[k]) (void)hipFree(s.f[k]);
             if (s.obst) (void)hipFree(s.obst);
+            if (s.obst_g) (void)hipFree(s.obst_g);
             if (s.partials) (void)hipFree(s.partials);
             if (s.partials2) (void)hipFree(s.partials2);
             if (s.av_local) (void)hipFree(s.av_local);

@@ -46,8 +46,8 @@ hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t
 hipError_t launch_stream(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
 hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s);
 hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n);
-hipError_t launch_stream2d(const StreamArgs &a, int blocks, int steps, bool reduce, int pd, hipStream_t s);
-hipError_t stream2d_blocks_per_cu(int steps, int pd, int &n);
+hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, hipStream_t s);
+hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
@@ -190,12 +190,13 @@ struct lbm_handle {
     int gr = 2;              // ghost ring width
     int stream_s = 4;        // LBM_STREAM_S: steps per stream launch when not configured
     int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
-    int stream_v = 2;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32),
+    int stream_v = 3;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32),
                              // 3 = two columns per lane without the streaming order's redundant work
     int og = 4;              // ghost width of the obstacle map
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     int stream_waves = 2;    // LBM_STREAM_W: register target of the two-column kernel (waves per SIMD)
-    int stream_pd = 2;       // LBM_STREAM_PD: v3 prefetch distance in rows (1 or 2)
+    int stream_cfg = 2;      // LBM_STREAM_CFG (v3): 0 one wave per workgroup; 1 four waves (adjacent strips);
+                             // 2 four waves + non-temporal lattice stores
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
@@ -258,7 +259,7 @@ struct lbm_handle {
         stream_hs = std::max(0, env_int("LBM_STREAM_HS", stream_hs));
         stream_v = std::min(std::max(env_int("LBM_STREAM_V", stream_v), 1), 3);
         stream_waves = env_int("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
-        stream_pd = env_int("LBM_STREAM_PD", stream_pd) == 1 ? 1 : 2;
+        stream_cfg = std::min(std::max(env_int("LBM_STREAM_CFG", stream_cfg), 0), 2);
         stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
             const char *g = getenv("LBM_STREAM_GUIDE");
@@ -613,7 +614,7 @@ struct lbm_handle {
             // (profiles/r01/stream/ab_hs_rounds.log).  Eight rounds where the
             // segments stay at least 4S rows high, fewer otherwise.
             int per_cu = 0, cus = 0;
-            const hipError_t occ = stream_v == 3 ? stream2d_blocks_per_cu(S, stream_pd, per_cu)
+            const hipError_t occ = stream_v == 3 ? stream2d_blocks_per_cu(S, stream_cfg, per_cu)
                                                  : stream2c_blocks_per_cu(S, stream_waves, per_cu);
             if (stream_v >= 2 && occ == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev) == hipSuccess &&
@@ -1269,7 +1270,7 @@ struct lbm_handle {
             if (n <= 0) return hipSuccess;
             const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
             if (stream_v == 1) return launch_stream(a, n, spl, interior, st);
-            if (stream_v == 3) return launch_stream2d(a, n, spl, interior, stream_pd, st);
+            if (stream_v == 3) return launch_stream2d(a, n, spl, interior, stream_cfg, st);
             return launch_stream2c(a, n, spl, interior, stream_waves, st);
         }
         if (fused_launch) {

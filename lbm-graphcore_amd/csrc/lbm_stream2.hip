@@ -246,7 +246,7 @@ __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2
     ob[1] = ocn[1];
 }
 
-template <int S, int PAR, bool GUARD, int PD>
+template <int S, int PAR, bool GUARD, int PD, bool NT>
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j) {
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
     if (PD == 1) stream2d_load<PD>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
@@ -291,7 +291,13 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
                 float *w0 = a.fout + (long long)y * g.pitch + g.xa;
                 if (g.owna && g.ownb) {
 #pragma unroll
-                    for (int k = 0; k < Q; ++k) *reinterpret_cast<f2 *>(w0 + k * g.P) = o[k];
+                    for (int k = 0; k < Q; ++k) {
+                        f2 *pd = reinterpret_cast<f2 *>(w0 + k * g.P);
+                        if (NT)
+                            __builtin_nontemporal_store(o[k], pd);
+                        else
+                            *pd = o[k];
+                    }
                 } else if (g.owna) {
 #pragma unroll
                     for (int k = 0; k < Q; ++k) w0[k * g.P] = o[k].x;
@@ -318,7 +324,7 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
 }
 
 // One work unit (strip x segment t) of the launch; accumulates |u| per level into st.tot.
-template <int S, int PD>
+template <int S, int PD, bool NT>
 __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st) {
     const int r = rect_of(a.rect_begin, t);
     const SRect R = a.rect[r];
@@ -355,15 +361,15 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     int j = g.j0;
 #pragma unroll 1
     for (int i = 0; i < S; ++i, j += 2) {
-        stream2d_row<S, 0, true, PD>(a, g, st, j);
-        stream2d_row<S, 1, true, PD>(a, g, st, j + 1);
+        stream2d_row<S, 0, true, PD, NT>(a, g, st, j);
+        stream2d_row<S, 1, true, PD, NT>(a, g, st, j + 1);
     }
 #pragma unroll 1
     for (; j + 1 <= g.jlast; j += 2) {
-        stream2d_row<S, 0, false, PD>(a, g, st, j);
-        stream2d_row<S, 1, false, PD>(a, g, st, j + 1);
+        stream2d_row<S, 0, false, PD, NT>(a, g, st, j);
+        stream2d_row<S, 1, false, PD, NT>(a, g, st, j + 1);
     }
-    if (j <= g.jlast) stream2d_row<S, 0, false, PD>(a, g, st, j);
+    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT>(a, g, st, j);
 }
 
 // |u| partials of one work unit, one per level (= time step of the launch)
@@ -379,58 +385,68 @@ __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, 
     }
 }
 
-// One work unit per wave, t = xcd_remap(blockIdx) (blocks b and b+8 share an
-// XCD and take neighbouring units, so the strips' overlap columns are read
-// through one L2).  (A persistent grid taking units from a device-scope
-// counter balanced the waves better but read 1.30x the algorithmic bytes
-// instead of 1.18x: neighbouring strips landed on different XCDs.)
-template <int S, bool kReduce, int PD, int MINW>
-__global__ __launch_bounds__(64, MINW) void stream_steps2d(StreamArgs a) {
-    __shared__ float lds[1];
-    if (kReduce && blockIdx.x == 0) reduce_pending_n<64>(a.ctl, a.partials_prev, a.av_local, lds);
+// Work units: W waves per workgroup take W consecutive units (adjacent strips
+// of one segment row, so they run side by side on one CU and read their
+// shared overlap columns through its L1 / L2); t = xcd_remap(blockIdx) * W +
+// wave, and blocks b and b+8 share an XCD and take neighbouring units.  NT:
+// non-temporal lattice stores (the output is not read again by this launch).
+// tools/micro/stream_pattern.hip, the kernel's memory pattern alone at
+// 8192^2: 1.245 ms per pass with one wave per workgroup and plain stores,
+// 1.172 with four waves, 1.187 with nt stores, 1.121 with both.
+// (A persistent grid taking units from a device-scope counter balanced the
+// waves better but read 1.30x the algorithmic bytes instead of 1.18x:
+// neighbouring strips landed on different XCDs.)
+template <int S, bool kReduce, int W, bool NT>
+__global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
+    __shared__ float lds[W];
+    if (kReduce && blockIdx.x == 0) reduce_pending_n<64 * W>(a.ctl, a.partials_prev, a.av_local, lds);
 
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     Stream2State<S> st;
 #pragma unroll
     for (int l = 0; l < S; ++l) st.tot[l] = mk2(0.f);
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6);
     const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (t < a.total) stream2d_unit<S, PD>(a, t, lane, st);
-    stream2d_partials<S>(a, blockIdx.x, lane, st);
-    if (a.trace && lane == 0) {
+    if (t < a.total) stream2d_unit<S, 1, NT>(a, t, lane, st);
+    if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
+    if (a.trace && lane == 0 && t < a.total) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        a.trace[2 * (long long)blockIdx.x] = t_start;
-        a.trace[2 * (long long)blockIdx.x + 1] = t_end;
+        a.trace[2 * (long long)t] = t_start;
+        a.trace[2 * (long long)t + 1] = t_end;
     }
-    if (kReduce && blockIdx.x == 0 && lane == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
+    if (kReduce && blockIdx.x == 0 && threadIdx.x == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
 }
 
-template <int S, int PD>
-static void launch_s2d(const StreamArgs &a, int blocks, bool reduce, hipStream_t s) {
+template <int S, int W, bool NT>
+static void launch_s2d(const StreamArgs &a, int units, bool reduce, hipStream_t s) {
+    const int blocks = (units + W - 1) / W;
     if (reduce)
-        hipLaunchKernelGGL((stream_steps2d<S, true, PD, 2>), dim3(blocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, true, W, NT>), dim3(blocks), dim3(64 * W), 0, s, a);
     else
-        hipLaunchKernelGGL((stream_steps2d<S, false, PD, 2>), dim3(blocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, false, W, NT>), dim3(blocks), dim3(64 * W), 0, s, a);
 }
 
-hipError_t stream2d_blocks_per_cu(int steps, int pd, int &n) {
-    const void *fn = pd == 2 ? (steps == 2   ? (const void *)&stream_steps2d<2, false, 2, 2>
-                                : steps == 3 ? (const void *)&stream_steps2d<3, false, 2, 2>
-                                             : (const void *)&stream_steps2d<4, false, 2, 2>)
-                             : (steps == 2   ? (const void *)&stream_steps2d<2, false, 1, 2>
-                                : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, 2>
-                                             : (const void *)&stream_steps2d<4, false, 1, 2>);
+// waves per CU of the configuration (cfg: 0 = one wave per workgroup, plain
+// stores; 1 = four waves, plain; 2 = four waves, nt stores)
+hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n) {
+    const void *fn = steps == 2 ? (const void *)&stream_steps2d<2, false, 1, false>
+                   : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false>
+                                : (const void *)&stream_steps2d<4, false, 1, false>;
+    (void)cfg;  // same registers per wave in every configuration: count waves of the one-wave form
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, 0);
 }
 
-hipError_t launch_stream2d(const StreamArgs &a, int blocks, int steps, bool reduce, int pd, hipStream_t s) {
-    switch (steps * 10 + pd) {
-        case 21: launch_s2d<2, 1>(a, blocks, reduce, s); break;
-        case 31: launch_s2d<3, 1>(a, blocks, reduce, s); break;
-        case 41: launch_s2d<4, 1>(a, blocks, reduce, s); break;
-        case 22: launch_s2d<2, 2>(a, blocks, reduce, s); break;
-        case 32: launch_s2d<3, 2>(a, blocks, reduce, s); break;
-        case 42: launch_s2d<4, 2>(a, blocks, reduce, s); break;
+hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, hipStream_t s) {
+    switch (steps * 10 + cfg) {
+        case 20: launch_s2d<2, 1, false>(a, units, reduce, s); break;
+        case 30: launch_s2d<3, 1, false>(a, units, reduce, s); break;
+        case 40: launch_s2d<4, 1, false>(a, units, reduce, s); break;
+        case 21: launch_s2d<2, 4, false>(a, units, reduce, s); break;
+        case 31: launch_s2d<3, 4, false>(a, units, reduce, s); break;
+        case 41: launch_s2d<4, 4, false>(a, units, reduce, s); break;
+        case 22: launch_s2d<2, 4, true>(a, units, reduce, s); break;
+        case 32: launch_s2d<3, 4, true>(a, units, reduce, s); break;
+        case 42: launch_s2d<4, 4, true>(a, units, reduce, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

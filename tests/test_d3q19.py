@@ -203,3 +203,35 @@ def test_d3q19_512cube_64bit_indexing(gpu_lib, monkeypatch):
     assert np.isfinite(a[::31, ::29, ::37]).all()
     assert np.array_equal(a, b)
     np.testing.assert_allclose(av_a, av_b, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,seg", [(2, "64"), (3, "4"), (4, "3"), (5, "1"), (8, "64")])
+@pytest.mark.parametrize("steps", [8, 9])
+def test_d3q19_slabs_two_step_bitwise(gpu_lib, parts, seg, steps, monkeypatch):
+    """Two steps per pass on z slabs (BASELINE config 5's 8-slab form): each pass
+    computes the two boundary plane pairs first, exchanges them (all 19 speeds of
+    two planes each way) and then the interior; odd step counts end with a
+    one-step launch.  Ragged slabs of 5..20 planes, z segments of 1..64 planes."""
+    monkeypatch.setenv("LBM3D_SEG", seg)
+    p, obst, c0 = _problem(22, 9, 40, 100 + parts)
+    ref, ref_av = oracle.run3d(p, obst, steps, c0)
+    cells, av = _gpu3d(gpu_lib, p, obst, c0, steps, parts=parts, devices=[0])
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+    monkeypatch.setenv("LBM3D_TWO", "0")  # the one-step slab path gives the same lattice
+    cells1, _ = _gpu3d(gpu_lib, p, obst, c0, steps, parts=parts, devices=[0])
+    assert np.array_equal(cells1, ref)
+
+
+@pytest.mark.gpu
+def test_d3q19_rccl_two_step_self_exchange_bitwise(gpu_lib):
+    """World of one over RCCL with the two-step pass: the two-plane ghost pairs go
+    through ncclSend / ncclRecv to itself, twice per pass, in the engine's order."""
+    p, obst, c0 = _problem(24, 10, 12, 17)
+    for steps in (6, 7):
+        ref, ref_av = oracle.run3d(p, obst, steps, c0)
+        cells, av = _gpu3d(gpu_lib, p, obst, c0, steps, transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1,
+                           devices=[0], unique_id=gpu_lib.rccl_unique_id())
+        assert np.array_equal(cells, ref)
+        np.testing.assert_allclose(av, ref_av, rtol=1e-5)

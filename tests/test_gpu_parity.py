@@ -600,3 +600,26 @@ def test_local_load_store_matches_full(gpu_lib, parts, grid):
         assert np.array_equal(b, ref[y0:y0 + h, x0:x0 + w])
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
     assert np.array_equal(av, av_full)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, monkeypatch):
+    """The v3 stream kernel's launch forms (LBM_STREAM_CFG: one wave per
+    workgroup; four waves taking adjacent strips; four waves with non-temporal
+    lattice stores) and its guided segment tiers: bitwise vs the oracle on a
+    single domain, 2x2 and 1x3 loop-back, and with one-step remainders."""
+    monkeypatch.setenv("LBM_STREAM_V", "3")
+    monkeypatch.setenv("LBM_STREAM_CFG", str(cfg))
+    monkeypatch.setenv("LBM_STREAM_GUIDE", "24:0.6,8:0.3,3")
+    rng = np.random.default_rng(cfg)
+    p = lio.Params(300, 260, 9, 10, 0.1, 0.02, 1.7)
+    obst = (rng.random((260, 300)) < 0.03).astype(np.uint8)
+    cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((260, 300, 9)))).astype(np.float32)
+    for steps in (8, 9):
+        ref, ref_av = oracle.run(p, obst, steps, cells0)
+        for kw in (dict(), dict(parts=4, grid=(2, 2)), dict(parts=3, grid=(1, 3))):
+            cells, av, used = gpu_run(gpu_lib, p, obst, cells0, steps, devices=[0], kernel=gpu_lib.KERNEL_STREAM,
+                                      steps_per_launch=4, **kw)
+            assert used == "stream"
+            assert np.array_equal(cells, ref), (steps, kw)
+            np.testing.assert_allclose(av, ref_av, rtol=1e-5)

@@ -1,0 +1,159 @@
+// stream_pattern.hip -- HBM rate of the register-streaming kernels' memory
+// pattern with the arithmetic removed (or replaced by a tunable amount of
+// independent packed-fp32 work), to separate "the access pattern's own
+// bandwidth ceiling" from "compute / memory overlap" for lbm_stream2.hip.
+//
+// Lattice: row-interleaved SoA like the engine, f[y][k][x] (9 planes of a row
+// adjacent), 8192^2 cells, plane row = RF floats.  One wave walks a strip of
+// 64*V columns (V floats per lane: 2 = the stream kernel's float2, 4 =
+// float4) over a segment of HS rows plus 2*S re-streamed rows, loading the
+// nine plane chunks of every row (prefetched one row ahead) and storing the
+// owned columns of row j-S to the second lattice.  Strips overlap by 2*S
+// columns, as in the kernel.  WORK = packed-fp32 FMAs per lane per row (the
+// real kernel issues ~430 packed ops per row at S = 4).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o stream_pattern stream_pattern.hip && ./stream_pattern
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int NX = 8192, NY = 8192, S = 4, Q = 9;
+constexpr int XOFF = 64, GR = 4;
+constexpr int RF = ((NX + XOFF + GR + 2 + 63) / 64) * 64;  // floats per plane row
+constexpr long long PITCH = (long long)Q * RF;             // floats per lattice row
+
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int xcd = b & 7;
+    const int q = nb >> 3, r = nb & 7;
+    const int start = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return start + (b >> 3);
+}
+
+template <int V>
+struct Vec;
+template <>
+struct Vec<2> { typedef f2 T; };
+template <>
+struct Vec<4> { typedef f4 T; };
+
+// LAYOUT 0: f[y][k][x] (row-interleaved, the engine's); 1: f[k][y][x] (planar).
+// W waves per workgroup take W adjacent strips (co-scheduled on one CU).
+// NT: non-temporal stores.
+template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1>
+__global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin, float *__restrict__ fout, int hs,
+                                                  int nstrip, int total, float *sink) {
+    typedef typename Vec<V>::T T;
+    const long long PS = LAYOUT == 0 ? PITCH : RF;                       // row stride
+    const long long KS = LAYOUT == 0 ? RF : (long long)(NY + 2 * GR) * RF;  // plane stride
+    const int t = xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6);
+    if (t >= total) return;
+    const int lane = threadIdx.x & 63;
+    const int ow = 64 * V - 2 * S;
+    const int seg = t / nstrip, strip = t - seg * nstrip;
+    const int xo0 = strip * ow, xo1 = min(xo0 + ow, NX);
+    const int base = ((xo0 - S) & ~(V - 1));
+    const int xa = base + V * lane;
+    const bool own = xa >= xo0 && xa + V - 1 < xo1;
+    const int yo0 = seg * hs, yo1 = min(yo0 + hs, NY);
+    const float *src = fin + (long long)GR * PS + XOFF + xa;
+    float *dst = fout + (long long)GR * PS + XOFF + xa;
+    extern __shared__ float occupancy_limiter[];
+    if (hs < 0) occupancy_limiter[threadIdx.x] = 0.f;  // never: keeps the dynamic LDS request
+    T v[Q], nv[Q], nv2[Q];
+    int j = yo0 - S;
+    const int jl = yo1 + S - 1;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const T *>(src + (long long)j * PS + (long long)k * KS);
+    if (PD == 2) {
+#pragma unroll
+        for (int k = 0; k < Q; ++k) nv2[k] = *reinterpret_cast<const T *>(src + (long long)min(j + 1, jl) * PS + (long long)k * KS);
+    }
+    f2 acc[4] = {f2{0.f, 0.f}, f2{1.f, 1.f}, f2{2.f, 2.f}, f2{3.f, 3.f}};
+    for (; j <= jl; ++j) {
+        const int jn = min(j + PD, jl);
+        if (PD == 2) {
+#pragma unroll
+            for (int k = 0; k < Q; ++k) nv[k] = nv2[k];
+        }
+#pragma unroll
+        for (int k = 0; k < Q; ++k) (PD == 2 ? nv2[k] : nv[k]) = *reinterpret_cast<const T *>(src + (long long)jn * PS + (long long)k * KS);
+        // stand-in arithmetic: WORK independent packed FMAs per lane
+#pragma unroll
+        for (int w = 0; w < WORK; ++w) acc[w & 3] = __builtin_elementwise_fma(acc[w & 3], f2{1.0001f, 0.9999f}, f2{v[w % Q][0], v[(w + 1) % Q][1]});
+        const int y = j - S;
+        if (y >= yo0 && own) {
+#pragma unroll
+            for (int k = 0; k < Q; ++k) {
+                T o = v[k];
+                o[0] += acc[k & 3][0] * 0.0f;
+                T *pd = reinterpret_cast<T *>(dst + (long long)y * PS + (long long)k * KS);
+                if (NT)
+                    __builtin_nontemporal_store(o, pd);
+                else
+                    *pd = o;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < Q; ++k) v[k] = nv[k];
+    }
+    if (acc[0][0] == 12345.f) sink[0] = acc[1][1] + acc[2][0] + acc[3][1];
+}
+
+template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1>
+void run(const char *name, float *a, float *b, int hs, float *sink, int waves_per_simd = 0) {
+    // waves_per_simd > 0: dynamic LDS so that only that many waves fit per SIMD
+    const size_t lds = waves_per_simd > 0 ? (size_t)(160 * 1024) / (4 * waves_per_simd) * W - 256 : 0;
+    const int ow = 64 * V - 2 * S;
+    const int nstrip = (NX + ow - 1) / ow, nseg = (NY + hs - 1) / hs, total = nstrip * nseg;
+    const int blocks = (total + W - 1) / W;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int i = 0; i < 20; ++i)
+        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD>), dim3(blocks), dim3(64 * W), lds, 0, a, b, hs, nstrip, total,
+                           sink);
+    const int reps = 40;
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD>), dim3(blocks), dim3(64 * W), lds, 0, (i & 1) ? b : a,
+                           (i & 1) ? a : b, hs, nstrip, total, sink);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    ms /= reps;
+    const double lattice = 72.0 * NX * NY;                                      // algorithmic bytes per pass
+    const double moved = 36.0 * NX * NY * ((double)(hs + 2 * S) / hs) * (64.0 * V / ow) + 36.0 * NX * NY;
+    printf("{\"variant\": \"%s\", \"V\": %d, \"hs\": %d, \"work\": %d, \"waves\": %d, \"waves_per_simd\": %d, "
+           "\"ms\": %.4f, \"lattice_TBps\": %.3f, \"moved_TBps\": %.3f, \"err\": \"%s\"}\n",
+           name, V, hs, WORK, total, waves_per_simd, ms, lattice / ms / 1e9, moved / ms / 1e9,
+           hipGetErrorString(hipGetLastError()));
+}
+
+int main() {
+    const size_t n = (size_t)(NY + 2 * GR) * PITCH;
+    float *a = nullptr, *b = nullptr, *sink = nullptr;
+    if (hipMalloc(&a, n * 4) != hipSuccess || hipMalloc(&b, n * 4) != hipSuccess || hipMalloc(&sink, 64) != hipSuccess) {
+        fprintf(stderr, "alloc failed\n");
+        return 1;
+    }
+    (void)hipMemset(a, 0, n * 4);
+    (void)hipMemset(b, 0, n * 4);
+    // occupancy-matched to the stream kernel (2 waves per SIMD)
+    run<2, 0>("f2_hs35_o2", a, b, 35, sink, 2);
+    run<2, 0, 0, 4>("f2_hs35_w4_o2", a, b, 35, sink, 2);
+    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o2", a, b, 35, sink, 2);
+    run<2, 0, 0, 1, false, 2>("f2_hs35_pd2_o2", a, b, 35, sink, 2);
+    run<2, 0, 0, 4, true, 2>("f2_hs35_w4_nt_pd2_o2", a, b, 35, sink, 2);
+    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o3", a, b, 35, sink, 3);
+    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o4", a, b, 35, sink, 4);
+    run<2, 0>("f2_hs35_o8", a, b, 35, sink, 0);
+    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o8", a, b, 35, sink, 0);
+    run<2, 384, 0, 4, true>("f2_hs35_w4_nt_work384_o2", a, b, 35, sink, 2);
+    run<2, 384>("f2_hs35_work384_o2", a, b, 35, sink, 2);
+    return 0;
+}
