@@ -1,18 +1,22 @@
 #!/bin/bash
-# One GPU call (gpurun): the round's verification -- GPU tests, smoke, bench,
-# rocprofv3 kernel trace of the bench, and the two PMC passes (FETCH_SIZE,
-# WRITE_SIZE in separate runs) for the default kernel's HBM traffic.
+# One GPU call (gpurun): the round's verification -- GPU tests, smoke, the
+# driver's exact bench command and the default bench, a rocprofv3 kernel trace
+# of the driver's command, and the PMC passes (FETCH_SIZE, WRITE_SIZE and the
+# SQ counters, each in its own run) of the default kernel at 8192^2.
 #   /usr/local/graft/bin/gpurun --timeout 1500 -- bash tools/gpu_round.sh
 # then: python3 tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch/fetch_counter_collection.csv \
-#         --write gpurun_out/pmc_write/write_counter_collection.csv --kernel "stream_steps2c<4" \
+#         --write gpurun_out/pmc_write/write_counter_collection.csv --kernel "stream_steps2d<4" \
 #         --key 8192x8192/stream4 --cells 67108864 --out profiles/traffic.json
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE"
 bash tools/gpu_steps.sh \
   "900|pytest_gpu|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
   "300|smoke|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "400|bench|python bench.py" \
-  "300|prof_trace|rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o bench --output-format csv -- python3 bench.py --steps 400 --no-cpu-baseline --no-aux" \
+  "400|bench_drv|python3 bench.py --gpus 1 --steps 20 --warmup 5" \
+  "400|bench|python3 bench.py --no-cpu-baseline" \
+  "300|prof_trace|rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o drv --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-aux" \
   "120|pmc_fetch|timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1" \
-  "120|pmc_write|timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1"
-grep -h "passed\|failed" gpurun_out/pytest_gpu.log; tail -2 gpurun_out/smoke.log; tail -1 gpurun_out/bench.log
+  "120|pmc_write|timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1" \
+  "120|pmc_sq|timeout -s KILL 100 rocprofv3 --pmc $SQ -d gpurun_out/pmc_sq -o sq --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 40 --warmup 4 --rounds 1"
+grep -h "passed\|failed" gpurun_out/pytest_gpu.log; tail -n 2 gpurun_out/smoke.log; tail -n 1 gpurun_out/bench.log
