@@ -188,14 +188,14 @@ struct lbm_handle {
     int spl = 2;             // steps per fused launch
     int hw = 2;              // WG halo width (= spl)
     int gr = 2;              // ghost ring width
-    int stream_s = 4;        // LBM_STREAM_S: steps per stream launch when not configured
+    int stream_s = 5;        // LBM_STREAM_S: steps per stream launch when not configured (v1 / v2 kernels: at most 4)
     int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
     int stream_v = 3;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32),
                              // 3 = two columns per lane without the streaming order's redundant work
     int og = 4;              // ghost width of the obstacle map
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     int stream_waves = 2;    // LBM_STREAM_W: register target of the two-column kernel (waves per SIMD)
-    int stream_cfg = 2;      // LBM_STREAM_CFG (v3): 0 one wave per workgroup; 1 four waves (adjacent strips);
+    int stream_cfg = 0;      // LBM_STREAM_CFG (v3): 0 one wave per workgroup; 1 four waves (adjacent strips);
                              // 2 four waves + non-temporal lattice stores
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
@@ -255,7 +255,7 @@ struct lbm_handle {
         fused = env_int("LBM_TWO_STEP", fused ? 1 : 0) != 0;
         tile2 = std::min(std::max(env_int("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
         xoff = std::max(MAX_GR, (env_int("LBM_XOFF", xoff) + 3) / 4 * 4);
-        stream_s = std::min(std::max(env_int("LBM_STREAM_S", stream_s), 2), 4);
+        stream_s = std::min(std::max(env_int("LBM_STREAM_S", stream_s), 2), 6);
         stream_hs = std::max(0, env_int("LBM_STREAM_HS", stream_hs));
         stream_v = std::min(std::max(env_int("LBM_STREAM_V", stream_v), 1), 3);
         stream_waves = env_int("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
@@ -263,7 +263,7 @@ struct lbm_handle {
         stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
             const char *g = getenv("LBM_STREAM_GUIDE");
-            std::string spec = g ? std::string(g) : std::string("72:0.85,24:0.1,8");
+            std::string spec = g ? std::string(g) : std::string("96:0.85,32:0.1,10");
             guide.clear();
             if (spec != "0") {
                 size_t pos = 0;
@@ -762,10 +762,11 @@ struct lbm_handle {
         }
         // register-streaming kernel: S steps per launch, S-wide ghost ring;
         // every sub-domain at least S cells (2S across a decomposed dimension)
-        const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch : stream_s;
-        if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > 4))
-            throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2..4");
-        bool can_stream = fused && S >= 2 && S <= 4, big = true;
+        const int s_max = stream_v == 3 ? 6 : 4;  // the v3 kernel takes up to 6 steps per launch
+        const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch : std::min(stream_s, s_max);
+        if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
+            throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max));
+        bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;
             if (r.w < mw || r.h < mh) can_stream = false;

@@ -215,7 +215,7 @@ template <int S>
 struct Stream2State {
     f2 c0[S], c1[S], c3[S];          // planes 0, 1, 3 of row y (level L input)
     f2 p2[2][S], p5[2][S], p6[2][S]; // [parity]: planes 2, 5(left2), 6(right2) of rows y-1 / y
-    f2 tot[S];
+    float tot[S];                    // per level: running sum of |u| over the wave's owned cells
     f2 v[2][Q];                      // [parity]: input row j (parity of j) / prefetched row j+1
     unsigned ob[2][2];               // [parity][A/B]: obstacle bytes of those rows
     unsigned oba, obb;               // per-lane obstacle bits of the last rows (bit L = row j-L)
@@ -284,7 +284,7 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         if (rowlive) {
             const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
             const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
-            st.tot[b] += f2{ua, ub};
+            st.tot[b] += ua + ub;
         }
         if (L == S) {
             if (rowlive && (g.owna || g.ownb)) {
@@ -377,11 +377,11 @@ template <int S>
 __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, int lane, Stream2State<S> &st) {
 #pragma unroll
     for (int l = 0; l < S; ++l) {
-        float sum = st.tot[l].x + st.tot[l].y;
+        float sum = st.tot[l];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
         if (lane == 0) a.partials_out[(long long)l * a.stride + idx] = sum;
-        st.tot[l] = mk2(0.f);
+        st.tot[l] = 0.f;
     }
 }
 
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     const int lane = threadIdx.x & 63;
     Stream2State<S> st;
 #pragma unroll
-    for (int l = 0; l < S; ++l) st.tot[l] = mk2(0.f);
+    for (int l = 0; l < S; ++l) st.tot[l] = 0.f;
     const int t = xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6);
     const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (t < a.total) stream2d_unit<S, 1, NT>(a, t, lane, st);
@@ -429,9 +429,11 @@ static void launch_s2d(const StreamArgs &a, int units, bool reduce, hipStream_t 
 // waves per CU of the configuration (cfg: 0 = one wave per workgroup, plain
 // stores; 1 = four waves, plain; 2 = four waves, nt stores)
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n) {
-    const void *fn = steps == 2 ? (const void *)&stream_steps2d<2, false, 1, false>
-                   : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false>
-                                : (const void *)&stream_steps2d<4, false, 1, false>;
+    const void *fn = steps == 2   ? (const void *)&stream_steps2d<2, false, 1, false>
+                     : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false>
+                     : steps == 5 ? (const void *)&stream_steps2d<5, false, 1, false>
+                     : steps == 6 ? (const void *)&stream_steps2d<6, false, 1, false>
+                                  : (const void *)&stream_steps2d<4, false, 1, false>;
     (void)cfg;  // same registers per wave in every configuration: count waves of the one-wave form
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, 0);
 }
@@ -447,6 +449,12 @@ hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduc
         case 22: launch_s2d<2, 4, true>(a, units, reduce, s); break;
         case 32: launch_s2d<3, 4, true>(a, units, reduce, s); break;
         case 42: launch_s2d<4, 4, true>(a, units, reduce, s); break;
+        case 50: launch_s2d<5, 1, false>(a, units, reduce, s); break;
+        case 51: launch_s2d<5, 4, false>(a, units, reduce, s); break;
+        case 52: launch_s2d<5, 4, true>(a, units, reduce, s); break;
+        case 60: launch_s2d<6, 1, false>(a, units, reduce, s); break;
+        case 61: launch_s2d<6, 4, false>(a, units, reduce, s); break;
+        case 62: launch_s2d<6, 4, true>(a, units, reduce, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

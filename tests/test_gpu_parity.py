@@ -32,7 +32,7 @@ def sha(cells):
     return hashlib.sha256(np.ascontiguousarray(cells, dtype="<f4").tobytes()).hexdigest()
 
 
-MODES = ["scalar", "vec4", "step2", "stream2", "stream3", "stream4"]
+MODES = ["scalar", "vec4", "step2", "stream2", "stream3", "stream4", "stream5"]
 # single-domain modes: the lattice-resident persistent kernel serves one sub-domain only
 SINGLE_MODES = MODES + ["resident"]
 
@@ -160,7 +160,7 @@ def test_decomposed_small_ragged(gpu_lib, parts, mode):
 # ------------------------------------------------ reference grids ----
 
 @pytest.mark.parametrize("grid", GRIDS)
-@pytest.mark.parametrize("mode", ["vec4", "step2", "stream4", "resident"])
+@pytest.mark.parametrize("mode", ["vec4", "step2", "stream4", "stream5", "resident"])
 def test_reference_grid_full_run(gpu_lib, grid, mode, tmp_path):
     """Full maxIters run: final lattice bitwise == oracle (sha256), av_vels ~ oracle,
     and the reference gate (check.py, 1 %) against check/*.dat passes."""
@@ -205,7 +205,7 @@ def test_determinism_and_rerun(gpu_lib):
     np.testing.assert_allclose(outs[0][1], av2, rtol=1e-4)
 
 
-@pytest.mark.parametrize("mode", ["step2", "stream4"])
+@pytest.mark.parametrize("mode", ["step2", "stream4", "stream5"])
 def test_large_grid_steps_and_conservation(gpu_lib, mode):
     """8192^2 (the roofline config): 4 steps bitwise vs oracle, then mass conserved over 200 steps."""
     n = 8192
@@ -253,7 +253,7 @@ def test_abi_errors(gpu_lib):
 
 @pytest.mark.parametrize("transport,parts,grid", [("local", 1, (1, 1)), ("rccl", 1, (1, 1)), ("local", 2, (1, 2)),
                                                   ("local", 4, (2, 2))])
-@pytest.mark.parametrize("mode", ["vec4", "step2", "stream3", "stream4"])
+@pytest.mark.parametrize("mode", ["vec4", "step2", "stream3", "stream4", "stream5"])
 def test_forced_exchange_bitwise(gpu_lib, transport, parts, grid, mode):
     """Every periodic wrap goes through the transport (self send/recv): the full
     boundary/exchange/unpack/interior schedule -- with real RCCL p2p calls in
@@ -361,13 +361,15 @@ def test_stream_size_limits(gpu_lib):
 
 
 @pytest.mark.parametrize("version", [1, 2, 3])
-@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4"])
+@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5"])
 def test_open_periodic_random_bitwise(gpu_lib, mode, version, monkeypatch):
     """No walls: flow crosses every periodic seam and every sub-domain seam.
     Random sparse obstacles, perturbed populations, odd sizes; single domain
     and 2x2 / 3x2 loop-back decompositions."""
     if mode == "step2" and version != 1:
         pytest.skip("one step2 variant")
+    if mode == "stream5" and version != 3:
+        pytest.skip("5 steps per launch: v3 kernel only")
     monkeypatch.setenv("LBM_STREAM_V", str(version))
     rng = np.random.default_rng(7)
     p = lio.Params(150, 70, 9, 10, 0.1, 0.02, 1.7)
@@ -550,7 +552,7 @@ def _adversarial_state(nx, ny, seed):
     return cells.astype(np.float32)
 
 
-@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "resident", "vec4", "step2"])
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "resident", "vec4", "step2"])
 @pytest.mark.parametrize("version", [2, 3])
 def test_division_adversarial_states_bitwise(gpu_lib, mode, version, monkeypatch):
     """lbm_packed.hpp's short division sequences (x/9, x/36 by multiply + two
@@ -561,6 +563,8 @@ def test_division_adversarial_states_bitwise(gpu_lib, mode, version, monkeypatch
     no obstacles and no acceleration (so the states stay in their binades)."""
     if version == 3 and not mode.startswith("stream"):
         pytest.skip("LBM_STREAM_V only selects the stream kernel")
+    if mode == "stream5" and version != 3:
+        pytest.skip("5 steps per launch: v3 kernel only")
     monkeypatch.setenv("LBM_STREAM_V", str(version))
     monkeypatch.setenv("LBM_RES_V", "2")  # the packed resident kernel (collide2)
     nx, ny = 256, 66
@@ -602,12 +606,14 @@ def test_local_load_store_matches_full(gpu_lib, parts, grid):
     assert np.array_equal(av, av_full)
 
 
+@pytest.mark.parametrize("S", [4, 5, 6])
 @pytest.mark.parametrize("cfg", [0, 1, 2])
-def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, monkeypatch):
+def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, S, monkeypatch):
     """The v3 stream kernel's launch forms (LBM_STREAM_CFG: one wave per
     workgroup; four waves taking adjacent strips; four waves with non-temporal
-    lattice stores) and its guided segment tiers: bitwise vs the oracle on a
-    single domain, 2x2 and 1x3 loop-back, and with one-step remainders."""
+    lattice stores), 4 to 6 steps per launch, and its guided segment tiers:
+    bitwise vs the oracle on a single domain, 2x2 and 1x3 loop-back, and with
+    one-step remainders."""
     monkeypatch.setenv("LBM_STREAM_V", "3")
     monkeypatch.setenv("LBM_STREAM_CFG", str(cfg))
     monkeypatch.setenv("LBM_STREAM_GUIDE", "24:0.6,8:0.3,3")
@@ -615,11 +621,11 @@ def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, monkeypatch):
     p = lio.Params(300, 260, 9, 10, 0.1, 0.02, 1.7)
     obst = (rng.random((260, 300)) < 0.03).astype(np.uint8)
     cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((260, 300, 9)))).astype(np.float32)
-    for steps in (8, 9):
+    for steps in (2 * S, 2 * S + 1):
         ref, ref_av = oracle.run(p, obst, steps, cells0)
         for kw in (dict(), dict(parts=4, grid=(2, 2)), dict(parts=3, grid=(1, 3))):
             cells, av, used = gpu_run(gpu_lib, p, obst, cells0, steps, devices=[0], kernel=gpu_lib.KERNEL_STREAM,
-                                      steps_per_launch=4, **kw)
+                                      steps_per_launch=S, **kw)
             assert used == "stream"
             assert np.array_equal(cells, ref), (steps, kw)
             np.testing.assert_allclose(av, ref_av, rtol=1e-5)

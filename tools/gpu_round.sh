@@ -5,8 +5,8 @@
 # SQ counters, each in its own run) of the default kernel at 8192^2.
 #   /usr/local/graft/bin/gpurun --timeout 1500 -- bash tools/gpu_round.sh
 # then: python3 tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch/fetch_counter_collection.csv \
-#         --write gpurun_out/pmc_write/write_counter_collection.csv --kernel "stream_steps2d<4" \
-#         --key 8192x8192/stream4 --cells 67108864 --out profiles/traffic.json
+#         --write gpurun_out/pmc_write/write_counter_collection.csv --kernel "stream_steps2d<5" \
+#         --key 8192x8192/stream5 --cells 67108864 --out profiles/traffic.json
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE"
