@@ -104,8 +104,12 @@ __device__ __forceinline__ void publish_pending(int *ctl, int steps, int n, int 
 
 // Store the nine populations of one cell at strip coordinates (sa, sb) of a
 // wide-halo destination (own ghost ring or send buffer, lbm_layout.hpp Dst2).
+// The destination is global memory: stores through a generic (flat) pointer
+// would make every later vmcnt wait a full drain (flat operations complete
+// out of order), including the prefetched rows of the stream kernels.
 __device__ __forceinline__ void store2(const Dst2 &d, int sa, int sb, const float (&o)[Q]) {
-    float *p = d.base + (long long)sa * d.s1 + (long long)sb * d.s2;
+    __attribute__((address_space(1))) float *p =
+        (__attribute__((address_space(1))) float *)d.base + (long long)sa * d.s1 + (long long)sb * d.s2;
 #pragma unroll
     for (int k = 0; k < Q; ++k) p[k * d.ks] = o[k];
 }

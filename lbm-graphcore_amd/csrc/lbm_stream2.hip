@@ -178,20 +178,55 @@ __global__ __launch_bounds__(64, MINW) void stream_steps2c(StreamArgs a) {
 
 // halo_out with the destinations read from device memory inside the (rare)
 // branch that stores them, so they hold no scalar registers across the loop
+typedef const __attribute__((address_space(4))) Dst2 CDst2;
+__device__ __forceinline__ Dst2 ld_dst(CDst2 *p) {
+    Dst2 d;
+    d.base = p->base;
+    d.ks = p->ks;
+    d.s1 = p->s1;
+    d.s2 = p->s2;
+    return d;
+}
+
 __device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, int y, const float (&o)[Q]) {
     const bool east = x >= a.w - S, west = x < S, north = y >= a.h - S, south = y < S;
-    const Dst2 *dg = a.dstg;
-    if (east) store2(dg[DE], x - (a.w - S), y, o);
-    if (west) store2(dg[DW], x, y, o);
+    // The table is launch-invariant: read through the constant address space
+    // under wave-uniform branches it becomes scalar loads, which never make
+    // the wave wait for its row prefetch (a vector load here would need a
+    // full vmcnt drain before its use).
+    CDst2 *dg = (CDst2 *)a.dstg;
+    const bool any_e = __builtin_amdgcn_ballot_w64(east) != 0, any_w = __builtin_amdgcn_ballot_w64(west) != 0;
+    if (any_e) {
+        const Dst2 d = ld_dst(dg + DE);
+        if (east) store2(d, x - (a.w - S), y, o);
+    }
+    if (any_w) {
+        const Dst2 d = ld_dst(dg + DW);
+        if (west) store2(d, x, y, o);
+    }
     if (north) {
-        store2(dg[DN], y - (a.h - S), x, o);
-        if (east) store2(dg[DNE], y - (a.h - S), x - (a.w - S), o);
-        if (west) store2(dg[DNW], y - (a.h - S), x, o);
+        const Dst2 d = ld_dst(dg + DN);
+        store2(d, y - (a.h - S), x, o);
+        if (any_e) {
+            const Dst2 e = ld_dst(dg + DNE);
+            if (east) store2(e, y - (a.h - S), x - (a.w - S), o);
+        }
+        if (any_w) {
+            const Dst2 w = ld_dst(dg + DNW);
+            if (west) store2(w, y - (a.h - S), x, o);
+        }
     }
     if (south) {
-        store2(dg[DS], y, x, o);
-        if (west) store2(dg[DSW], y, x, o);
-        if (east) store2(dg[DSE], y, x - (a.w - S), o);
+        const Dst2 d = ld_dst(dg + DS);
+        store2(d, y, x, o);
+        if (any_w) {
+            const Dst2 w = ld_dst(dg + DSW);
+            if (west) store2(w, y, x, o);
+        }
+        if (any_e) {
+            const Dst2 e = ld_dst(dg + DSE);
+            if (east) store2(e, y, x - (a.w - S), o);
+        }
     }
 }
 
@@ -405,7 +440,8 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     Stream2State<S> st;
 #pragma unroll
     for (int l = 0; l < S; ++l) st.tot[l] = 0.f;
-    const int t = xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6);
+    // wave-uniform: keeps the unit geometry and the row loop in scalar registers
+    const int t = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6));
     const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (t < a.total) stream2d_unit<S, 1, NT>(a, t, lane, st);
     if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
