@@ -48,6 +48,7 @@ hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool redu
 hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n);
 hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, hipStream_t s);
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n);
+hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, hipStream_t s);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
                              float w2, hipStream_t s);
@@ -173,6 +174,8 @@ struct Sub {
     float *pipe_partials = nullptr;         // PIPELINE: collision block partials
     Dst2 *dst2_dev = nullptr;               // [parity][8] stream-kernel halo destinations (StreamArgs::dstg)
     unsigned long long *trace = nullptr;    // LBM_STREAM_TRACE: per-wave timestamps of the last interior launch
+    uint8_t *uobst = nullptr;               // v3 per-unit obstacle flags: [interior units | boundary units]
+    int *uperm = nullptr;                   // v3 dispatch order: [interior | boundary]
 };
 
 }  // namespace
@@ -580,6 +583,52 @@ struct lbm_handle {
             sb.partials_out = s.partials[par] + s.n3_int;
             s.a3_int[par] = si;
             s.a3_bnd[par] = sb;
+        }
+        // v3: which work units read an obstacle cell (the rest run without
+        // rebound selects); obstacles and the work split are fixed from here on
+        const char *uo = getenv("LBM_STREAM_UOBST");
+        if (use_stream && stream_v == 3 && !(uo && atoi(uo) == 0)) {
+            if (s.uobst) HIP_CHECK(hipFree(s.uobst));
+            const int ni = std::max(0, s.a3_int[0].total), nb = std::max(0, s.a3_bnd[0].total);
+            HIP_CHECK(hipMalloc(&s.uobst, (size_t)ni + nb + 1));
+            HIP_CHECK(stream2d_unit_flags(s.a3_int[0], spl, s.uobst, s.s_comp));
+            HIP_CHECK(stream2d_unit_flags(s.a3_bnd[0], spl, s.uobst + ni, s.s_comp));
+            HIP_CHECK(hipStreamSynchronize(s.s_comp));
+            for (int par = 0; par < 2; ++par) {
+                s.a3_int[par].uobst = s.uobst;
+                s.a3_bnd[par].uobst = s.uobst + ni;
+            }
+            // dispatch order: within each XCD's range of slots (xcd_remap),
+            // the units that read obstacle cells (slower: rebound selects)
+            // first, the rest after, each group in its original order
+            const char *so = getenv("LBM_STREAM_ORDER");
+            if (!(so && atoi(so) == 0)) {
+                std::vector<uint8_t> fl((size_t)ni + nb);
+                HIP_CHECK(hipMemcpy(fl.data(), s.uobst, fl.size(), hipMemcpyDeviceToHost));
+                const int W = stream_cfg == 0 ? 1 : 4;
+                std::vector<int> perm((size_t)ni + nb);
+                auto order = [&](int off, int n) {
+                    const int blocks = (n + W - 1) / W, q = blocks / 8, r = blocks % 8;
+                    for (int x = 0; x < 8; ++x) {
+                        const int b0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+                        const int nbx = q + (x < r ? 1 : 0);
+                        const int t0 = std::min(n, b0 * W), t1 = std::min(n, (b0 + nbx) * W);
+                        int k = t0;
+                        for (int pass = 0; pass < 2; ++pass)
+                            for (int t = t0; t < t1; ++t)
+                                if ((fl[(size_t)off + t] != 0) == (pass == 0)) perm[(size_t)off + k++] = t;
+                    }
+                };
+                order(0, ni);
+                order(ni, nb);
+                if (s.uperm) HIP_CHECK(hipFree(s.uperm));
+                HIP_CHECK(hipMalloc(&s.uperm, sizeof(int) * (perm.size() + 1)));
+                HIP_CHECK(hipMemcpy(s.uperm, perm.data(), sizeof(int) * perm.size(), hipMemcpyHostToDevice));
+                for (int par = 0; par < 2; ++par) {
+                    s.a3_int[par].uperm = s.uperm;
+                    s.a3_bnd[par].uperm = s.uperm + ni;
+                }
+            }
         }
     }
 
@@ -1578,6 +1627,8 @@ struct lbm_handle {
             if (s.obst) (void)hipFree(s.obst);
             if (s.pipe_partials) (void)hipFree(s.pipe_partials);
             if (s.dst2_dev) (void)hipFree(s.dst2_dev);
+            if (s.uobst) (void)hipFree(s.uobst);
+            if (s.uperm) (void)hipFree(s.uperm);
             if (s.trace) (void)hipFree(s.trace);
             if (s.obst_g) (void)hipFree(s.obst_g);
             if (s.halo_mem) (void)hipFree(s.halo_mem);

@@ -161,6 +161,8 @@ struct StreamArgs {
     int rect_begin[MAX_SRECTS];
     Dst2 dst[8];            // WG halo destinations, g = S
     const Dst2 *dstg;       // the same eight in device memory (read only where a halo cell is stored)
+    const uint8_t *uobst;   // v3: per work unit, 1 = reads an obstacle cell (nullptr: every unit may)
+    const int *uperm;       // v3: dispatch slot -> work unit (nullptr: identity)
     unsigned long long *trace;  // diagnostics (LBM_STREAM_TRACE): per unit {start, end} s_memrealtime, or null
     float *partials_out;    // step s of this launch: partials_out[s*stride + blockIdx.x]
     const float *partials_prev;

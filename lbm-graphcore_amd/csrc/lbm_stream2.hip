@@ -269,31 +269,42 @@ struct Stream2Geo {
 // issued while row j is computed -- PD = 2 keeps two rows of every wave in
 // flight (the kernel is bound by the memory-level parallelism of two waves
 // per SIMD, not by VALU: tools/pmc_summary.py SQ_WAIT_ANY), at 18 more VGPRs.
-template <int PD>
+template <int PD, bool OBST>
 __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2Geo &g, int j, f2 (&v)[Q],
                                               unsigned (&ob)[2]) {
     const int jn = min(j, g.jlast);
     const float *cn = g.src + (long long)jn * g.pitch;
 #pragma unroll
     for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const f2 *>(cn + k * g.P);
-    const uint8_t *ocn = g.obp + (long long)(jn + a.og) * a.ogp;
-    ob[0] = ocn[0];
-    ob[1] = ocn[1];
+    if (OBST) {
+        const uint8_t *ocn = g.obp + (long long)(jn + a.og) * a.ogp;
+        ob[0] = ocn[0];
+        ob[1] = ocn[1];
+    }
 }
 
-template <int S, int PAR, bool GUARD, int PD, bool NT>
+// OBST = false: the work unit reads no obstacle cell (stream2d_flags), so the
+// obstacle bytes are neither loaded nor tracked and no level carries the
+// rebound selects (their merge cost ~18 register copies per cell pair).
+template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST>
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j) {
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
-    if (PD == 1) stream2d_load<PD>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
-    const unsigned voa = st.ob[PAR][0] != 0 ? 1u : 0u, vob = st.ob[PAR][1] != 0 ? 1u : 0u;
-    st.oba = (st.oba << 1) | voa;
-    st.obb = (st.obb << 1) | vob;
-    st.rob = (st.rob << 1) | (__builtin_amdgcn_ballot_w64((voa | vob) != 0) != 0 ? 1ull : 0ull);
+    if (PD == 1) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
+    if (OBST) {
+        const unsigned voa = st.ob[PAR][0] != 0 ? 1u : 0u, vob = st.ob[PAR][1] != 0 ? 1u : 0u;
+        st.oba = (st.oba << 1) | voa;
+        st.obb = (st.obb << 1) | vob;
+        st.rob = (st.rob << 1) | (__builtin_amdgcn_ballot_w64((voa | vob) != 0) != 0 ? 1ull : 0ull);
+    }
 
+    // keep the row's arithmetic between its own prefetch and the next row's:
+    // the scheduler would otherwise hoist the next row's first uses of its
+    // just-issued loads into this row (a full vmcnt wait one row early)
+    __builtin_amdgcn_sched_barrier(0);
     f2 cur[Q];
 #pragma unroll
     for (int k = 0; k < Q; ++k) cur[k] = st.v[PAR][k];
-    if (PD == 2) stream2d_load<PD>(a, g, j + 2, st.v[PAR], st.ob[PAR]);
+    if (PD == 2) stream2d_load<PD, OBST>(a, g, j + 2, st.v[PAR], st.ob[PAR]);
 #pragma unroll
     for (int L = 1; L <= S; ++L) {
         const int b = L - 1;
@@ -310,8 +321,8 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         if (GUARD && j < g.j0 + 2 * L) continue;  // inputs of this row were never loaded: result unused
 
         f2 o[Q];
-        const bool oa = (st.oba >> L) & 1u, ob = (st.obb >> L) & 1u;
-        const bool any_obst = (st.rob >> L) & 1ull;
+        const bool oa = OBST && ((st.oba >> L) & 1u), ob = OBST && ((st.obb >> L) & 1u);
+        const bool any_obst = OBST && ((st.rob >> L) & 1ull);
         int gy = a.gy0 + y;
         gy = gy < 0 ? gy + a.ny : (gy >= a.ny ? gy - a.ny : gy);
         const f2 usq = collide2u(s, o, oa, ob, any_obst, gy == a.accel_g, a.omega, a.omo, a.w1, a.w2);
@@ -358,9 +369,9 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
     }
 }
 
-// One work unit (strip x segment t) of the launch; accumulates |u| per level into st.tot.
-template <int S, int PD, bool NT>
-__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st) {
+// Geometry of work unit t (strip x segment) for this lane.
+template <int S>
+__device__ __forceinline__ Stream2Geo stream2d_geo(const StreamArgs &a, int t, int lane) {
     const int r = rect_of(a.rect_begin, t);
     const SRect R = a.rect[r];
     const int lt = t - a.rect_begin[r];
@@ -382,6 +393,13 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     g.obp = a.obst_g + (xca + a.og);
     g.j0 = g.yo0 - S;
     g.jlast = g.yo1 + S - 1;
+    return g;
+}
+
+// One work unit (strip x segment t) of the launch; accumulates |u| per level into st.tot.
+template <int S, int PD, bool NT, bool OBST>
+__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st) {
+    const Stream2Geo g = stream2d_geo<S>(a, t, lane);
 
 #pragma unroll
     for (int b = 0; b < S; ++b) {
@@ -390,21 +408,21 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     }
     st.oba = st.obb = 0;
     st.rob = 0;
-    stream2d_load<PD>(a, g, g.j0, st.v[0], st.ob[0]);
-    if (PD == 2) stream2d_load<PD>(a, g, g.j0 + 1, st.v[1], st.ob[1]);
+    stream2d_load<PD, OBST>(a, g, g.j0, st.v[0], st.ob[0]);
+    if (PD == 2) stream2d_load<PD, OBST>(a, g, g.j0 + 1, st.v[1], st.ob[1]);
     // warm-up: rows j0 .. j0+2S-1 (level L valid from j0+2L); jlast >= j0+2S
     int j = g.j0;
 #pragma unroll 1
     for (int i = 0; i < S; ++i, j += 2) {
-        stream2d_row<S, 0, true, PD, NT>(a, g, st, j);
-        stream2d_row<S, 1, true, PD, NT>(a, g, st, j + 1);
+        stream2d_row<S, 0, true, PD, NT, OBST>(a, g, st, j);
+        stream2d_row<S, 1, true, PD, NT, OBST>(a, g, st, j + 1);
     }
 #pragma unroll 1
     for (; j + 1 <= g.jlast; j += 2) {
-        stream2d_row<S, 0, false, PD, NT>(a, g, st, j);
-        stream2d_row<S, 1, false, PD, NT>(a, g, st, j + 1);
+        stream2d_row<S, 0, false, PD, NT, OBST>(a, g, st, j);
+        stream2d_row<S, 1, false, PD, NT, OBST>(a, g, st, j + 1);
     }
-    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT>(a, g, st, j);
+    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST>(a, g, st, j);
 }
 
 // |u| partials of one work unit, one per level (= time step of the launch)
@@ -441,9 +459,22 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
 #pragma unroll
     for (int l = 0; l < S; ++l) st.tot[l] = 0.f;
     // wave-uniform: keeps the unit geometry and the row loop in scalar registers
-    const int t = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6));
+    const int slot = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6));
+    // dispatch order -> work unit (a.uperm: per XCD range, obstacle-bearing
+    // units first, so the slower units never start last); partials and flags
+    // are indexed by unit, so the |u| sums do not depend on the order
+    typedef const __attribute__((address_space(4))) int CI32;
+    const int t = (a.uperm != nullptr && slot < a.total) ? ((CI32 *)a.uperm)[slot] : slot;
     const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (t < a.total) stream2d_unit<S, 1, NT>(a, t, lane, st);
+    if (t < a.total) {
+        // per-unit obstacle flag (launch-invariant; scalar load): units that
+        // read no obstacle cell run the select-free copy of the unit loop
+        typedef const __attribute__((address_space(4))) uint8_t CU8;
+        if (a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0)
+            stream2d_unit<S, 1, NT, true>(a, t, lane, st);
+        else
+            stream2d_unit<S, 1, NT, false>(a, t, lane, st);
+    }
     if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
@@ -451,6 +482,36 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
         a.trace[2 * (long long)t + 1] = t_end;
     }
     if (kReduce && blockIdx.x == 0 && threadIdx.x == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
+}
+
+// uobst[t] = 1 when work unit t loads any obstacle cell (rows j0 .. jlast of
+// its strip, the same bytes stream2d_load reads), else 0.  One wave per unit;
+// run once per launch plan (obstacles are fixed for the engine's lifetime).
+template <int S>
+__global__ __launch_bounds__(64) void stream2d_flags(StreamArgs a, uint8_t *uobst) {
+    const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    if (t >= a.total) return;
+    const Stream2Geo g = stream2d_geo<S>(a, t, (int)threadIdx.x);
+    unsigned any = 0;
+    for (int j = g.j0; j <= g.jlast; ++j) {
+        const uint8_t *ocn = g.obp + (long long)(j + a.og) * a.ogp;
+        any |= (unsigned)ocn[0] | (unsigned)ocn[1];
+    }
+    const bool hit = __builtin_amdgcn_ballot_w64(any != 0) != 0;
+    if (threadIdx.x == 0) uobst[t] = hit ? 1 : 0;
+}
+
+hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, hipStream_t s) {
+    if (a.total <= 0) return hipSuccess;
+    switch (steps) {
+        case 2: hipLaunchKernelGGL(stream2d_flags<2>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 3: hipLaunchKernelGGL(stream2d_flags<3>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 4: hipLaunchKernelGGL(stream2d_flags<4>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 5: hipLaunchKernelGGL(stream2d_flags<5>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 6: hipLaunchKernelGGL(stream2d_flags<6>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 template <int S, int W, bool NT>

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -40,15 +41,17 @@ struct Vec<2> { typedef f2 T; };
 template <>
 struct Vec<4> { typedef f4 T; };
 
-// LAYOUT 0: f[y][k][x] (row-interleaved, the engine's); 1: f[k][y][x] (planar).
+// LAYOUT 0: f[y][k][x] (row-interleaved, the engine's); 1: f[k][y][x] (planar);
+// 2: f[y][x/128][k][x%128] (row-interleaved blocks of 128 columns: one row of a
+// 128-column block = 9 x 512 B contiguous).
 // W waves per workgroup take W adjacent strips (co-scheduled on one CU).
 // NT: non-temporal stores.
-template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1>
+template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1, bool STORE = true>
 __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin, float *__restrict__ fout, int hs,
                                                   int nstrip, int total, float *sink) {
     typedef typename Vec<V>::T T;
-    const long long PS = LAYOUT == 0 ? PITCH : RF;                       // row stride
-    const long long KS = LAYOUT == 0 ? RF : (long long)(NY + 2 * GR) * RF;  // plane stride
+    const long long PS = LAYOUT == 1 ? RF : PITCH;                                            // row stride
+    const long long KS = LAYOUT == 0 ? RF : LAYOUT == 2 ? 128 : (long long)(NY + 2 * GR) * RF;  // plane stride
     const int t = xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6);
     if (t >= total) return;
     const int lane = threadIdx.x & 63;
@@ -59,8 +62,10 @@ __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin,
     const int xa = base + V * lane;
     const bool own = xa >= xo0 && xa + V - 1 < xo1;
     const int yo0 = seg * hs, yo1 = min(yo0 + hs, NY);
-    const float *src = fin + (long long)GR * PS + XOFF + xa;
-    float *dst = fout + (long long)GR * PS + XOFF + xa;
+    const int xg = XOFF + xa;
+    const long long xo = LAYOUT == 2 ? (long long)(xg >> 7) * (Q * 128) + (xg & 127) : xg;
+    const float *src = fin + (long long)GR * PS + xo;
+    float *dst = fout + (long long)GR * PS + xo;
     extern __shared__ float occupancy_limiter[];
     if (hs < 0) occupancy_limiter[threadIdx.x] = 0.f;  // never: keeps the dynamic LDS request
     T v[Q], nv[Q], nv2[Q];
@@ -85,7 +90,7 @@ __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin,
 #pragma unroll
         for (int w = 0; w < WORK; ++w) acc[w & 3] = __builtin_elementwise_fma(acc[w & 3], f2{1.0001f, 0.9999f}, f2{v[w % Q][0], v[(w + 1) % Q][1]});
         const int y = j - S;
-        if (y >= yo0 && own) {
+        if (STORE && y >= yo0 && own) {
 #pragma unroll
             for (int k = 0; k < Q; ++k) {
                 T o = v[k];
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin,
     if (acc[0][0] == 12345.f) sink[0] = acc[1][1] + acc[2][0] + acc[3][1];
 }
 
-template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1>
+template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1, bool STORE = true>
 void run(const char *name, float *a, float *b, int hs, float *sink, int waves_per_simd = 0) {
     // waves_per_simd > 0: dynamic LDS so that only that many waves fit per SIMD
     const size_t lds = waves_per_simd > 0 ? (size_t)(160 * 1024) / (4 * waves_per_simd) * W - 256 : 0;
@@ -114,12 +119,12 @@ void run(const char *name, float *a, float *b, int hs, float *sink, int waves_pe
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (int i = 0; i < 20; ++i)
-        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD>), dim3(blocks), dim3(64 * W), lds, 0, a, b, hs, nstrip, total,
+        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD, STORE>), dim3(blocks), dim3(64 * W), lds, 0, a, b, hs, nstrip, total,
                            sink);
     const int reps = 40;
     (void)hipEventRecord(e0);
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD>), dim3(blocks), dim3(64 * W), lds, 0, (i & 1) ? b : a,
+        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD, STORE>), dim3(blocks), dim3(64 * W), lds, 0, (i & 1) ? b : a,
                            (i & 1) ? a : b, hs, nstrip, total, sink);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
@@ -134,7 +139,39 @@ void run(const char *name, float *a, float *b, int hs, float *sink, int waves_pe
            hipGetErrorString(hipGetLastError()));
 }
 
-int main() {
+// plain float4 copy of n floats (grid-stride), the HBM ceiling for comparison
+__global__ __launch_bounds__(256) void copy4(const f4 *__restrict__ a, f4 *__restrict__ b, long long n4) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) b[i] = a[i];
+}
+__global__ __launch_bounds__(256) void read4(const f4 *__restrict__ a, float *sink, long long n4) {
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) acc += a[i];
+    if (acc[0] == 12345.f) sink[0] = acc[1] + acc[2] + acc[3];
+}
+static void run_copy(const char *name, float *a, float *b, size_t n, float *sink, bool read_only) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    const long long n4 = (long long)(n / 4);
+    const int blocks = 256 * 32;
+    for (int r = 0; r < 25; ++r) {
+        if (r == 5) (void)hipEventRecord(e0);
+        if (read_only)
+            hipLaunchKernelGGL(read4, dim3(blocks), dim3(256), 0, 0, (const f4 *)a, sink, n4);
+        else
+            hipLaunchKernelGGL(copy4, dim3(blocks), dim3(256), 0, 0, (const f4 *)a, (f4 *)b, n4);
+    }
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    ms /= 20;
+    const double bytes = (read_only ? 4.0 : 8.0) * (double)n;
+    printf("{\"variant\": \"%s\", \"ms\": %.4f, \"moved_TBps\": %.3f, \"err\": \"%s\"}\n", name, ms, bytes / ms / 1e9,
+           hipGetErrorString(hipGetLastError()));
+}
+
+int main(int argc, char **argv) {
     const size_t n = (size_t)(NY + 2 * GR) * PITCH;
     float *a = nullptr, *b = nullptr, *sink = nullptr;
     if (hipMalloc(&a, n * 4) != hipSuccess || hipMalloc(&b, n * 4) != hipSuccess || hipMalloc(&sink, 64) != hipSuccess) {
@@ -144,16 +181,45 @@ int main() {
     (void)hipMemset(a, 0, n * 4);
     (void)hipMemset(b, 0, n * 4);
     // occupancy-matched to the stream kernel (2 waves per SIMD)
-    run<2, 0>("f2_hs35_o2", a, b, 35, sink, 2);
-    run<2, 0, 0, 4>("f2_hs35_w4_o2", a, b, 35, sink, 2);
-    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o2", a, b, 35, sink, 2);
-    run<2, 0, 0, 1, false, 2>("f2_hs35_pd2_o2", a, b, 35, sink, 2);
-    run<2, 0, 0, 4, true, 2>("f2_hs35_w4_nt_pd2_o2", a, b, 35, sink, 2);
-    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o3", a, b, 35, sink, 3);
-    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o4", a, b, 35, sink, 4);
-    run<2, 0>("f2_hs35_o8", a, b, 35, sink, 0);
-    run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o8", a, b, 35, sink, 0);
-    run<2, 384, 0, 4, true>("f2_hs35_w4_nt_work384_o2", a, b, 35, sink, 2);
-    run<2, 384>("f2_hs35_work384_o2", a, b, 35, sink, 2);
+    const int which = argc > 1 ? atoi(argv[1]) : 0;
+    if (which == 0) {
+        run<2, 0>("f2_hs35_o2", a, b, 35, sink, 2);
+        run<2, 0, 0, 4>("f2_hs35_w4_o2", a, b, 35, sink, 2);
+        run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o2", a, b, 35, sink, 2);
+        run<2, 0, 0, 1, false, 2>("f2_hs35_pd2_o2", a, b, 35, sink, 2);
+        run<2, 0, 0, 4, true, 2>("f2_hs35_w4_nt_pd2_o2", a, b, 35, sink, 2);
+        run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o3", a, b, 35, sink, 3);
+        run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o4", a, b, 35, sink, 4);
+        run<2, 0>("f2_hs35_o8", a, b, 35, sink, 0);
+        run<2, 0, 0, 4, true>("f2_hs35_w4_nt_o8", a, b, 35, sink, 0);
+        run<2, 384, 0, 4, true>("f2_hs35_w4_nt_work384_o2", a, b, 35, sink, 2);
+        run<2, 384>("f2_hs35_work384_o2", a, b, 35, sink, 2);
+    } else if (which == 2) {
+        run_copy("copy4_lattice", a, b, n, sink, false);
+        run_copy("read4_lattice", a, b, n, sink, true);
+        run<2, 0, 0, 1, false, 1, false>("L0_hs96_o2_noStore", a, b, 96, sink, 2);
+        run<2, 0, 0, 1, false, 1, false>("L0_hs96_o8_noStore", a, b, 96, sink, 0);
+        run<2, 0, 0, 4, true>("L0_hs96_w4nt_o2", a, b, 96, sink, 2);
+        run<2, 0, 0, 4, true>("L0_hs96_w4nt_o8", a, b, 96, sink, 0);
+        run<4, 0, 0>("V4_hs96_o2", a, b, 96, sink, 2);
+        run<4, 0, 0>("V4_hs96_o8", a, b, 96, sink, 0);
+        run<2, 0, 0>("L0_hs400_o8", a, b, 400, sink, 0);
+        run<2, 0, 0>("L0_hs20_o8", a, b, 20, sink, 0);
+    } else {
+        // layouts: row-interleaved (0), planar (1), 128-column blocks (2); hs 35 and 96
+        run<2, 0, 0>("L0_hs35_o2", a, b, 35, sink, 2);
+        run<2, 0, 1>("L1_hs35_o2", a, b, 35, sink, 2);
+        run<2, 0, 2>("L2_hs35_o2", a, b, 35, sink, 2);
+        run<2, 0, 0>("L0_hs96_o2", a, b, 96, sink, 2);
+        run<2, 0, 1>("L1_hs96_o2", a, b, 96, sink, 2);
+        run<2, 0, 2>("L2_hs96_o2", a, b, 96, sink, 2);
+        run<2, 0, 2, 4, true>("L2_hs96_w4_nt_o2", a, b, 96, sink, 2);
+        run<2, 0, 0>("L0_hs96_o4", a, b, 96, sink, 4);
+        run<2, 0, 2>("L2_hs96_o4", a, b, 96, sink, 4);
+        run<2, 0, 0>("L0_hs96_o8", a, b, 96, sink, 0);
+        run<2, 0, 2>("L2_hs96_o8", a, b, 96, sink, 0);
+        run<2, 384, 2>("L2_hs96_work384_o2", a, b, 96, sink, 2);
+        run<2, 384, 0>("L0_hs96_work384_o2", a, b, 96, sink, 2);
+    }
     return 0;
 }
