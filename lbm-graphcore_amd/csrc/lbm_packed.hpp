@@ -117,10 +117,12 @@ __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bo
     return f2{oa ? 0.f : sqrt_av(usq.x), ob ? 0.f : sqrt_av(usq.y)};
 }
 
-// collide2 for a wave whose pair row is uniform: the folded acceleration is
-// applied only on the accelerated row (accrow, wave-uniform) exactly as
-// LastChance.cpp:253-261 does, and |u|^2 is returned for the caller to take
-// the square root only where the row counts towards av_vels.
+// collide2 for a wave whose pair row is uniform: the folded acceleration
+// accel * w is added on EVERY row, as LastChance.cpp:253-261 does (accel = 0
+// adds 0 * w, which turns a -0.0 population into +0.0 -- skipping the add off
+// the accelerated row would not), with accel * w formed on the scalar unit
+// (accrow is wave-uniform), and |u|^2 is returned for the caller to take the
+// square root only where the row counts towards av_vels.
 __device__ __forceinline__ f2 collide2u(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, bool accrow,
                                         float omega, float omo, float w1, float w2) {
     const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
@@ -146,8 +148,9 @@ __device__ __forceinline__ f2 collide2u(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
     const f2 ud = -ux + uy;
     c[6] = s[6] * OMO + ld2 * ((c45 * ud) * (c23 + ud) + csq);
     c[8] = s[8] * OMO + ld2 * ((n45 * ud) * (c23 - ud) + csq);
-    if (accrow) {
-        const f2 a1 = mk2(w1), a2 = mk2(w2);
+    {
+        const float accf = accrow ? 1.00f : 0.00f;
+        const f2 a1 = mk2(accf * w1), a2 = mk2(accf * w2);
         c[1] = c[1] + a1;
         c[3] = c[3] - a1;
         c[5] = c[5] + a2;

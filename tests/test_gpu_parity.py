@@ -583,6 +583,44 @@ def test_division_adversarial_states_bitwise(gpu_lib, mode, version, monkeypatch
                         f"gpu {cells[y, x, k]!r} oracle {ref[y, x, k]!r}")
 
 
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "resident", "vec4", "step2"])
+@pytest.mark.parametrize("version", [2, 3])
+def test_signed_zero_states_bitwise(gpu_lib, mode, version, monkeypatch):
+    """The folded acceleration is added on EVERY row as accel * w
+    (LastChance.cpp:253-261: + 0 * w1 off the accelerated row), which turns a
+    -0.0 post-collision population into +0.0.  A state whose density
+    underflows ld1 = rho / 9 * omega to +0 while |u|^2 is huge (csq < 0)
+    produces -0.0 populations on every row; a kernel that skipped the add off
+    the accelerated row would keep them negative.  Bitwise vs the oracle,
+    NaN positions equal (their payloads are not compared)."""
+    if version == 3 and not mode.startswith("stream"):
+        pytest.skip("LBM_STREAM_V only selects the stream kernel")
+    if mode == "stream5" and version != 3:
+        pytest.skip("5 steps per launch: v3 kernel only")
+    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    monkeypatch.setenv("LBM_RES_V", "2")
+    nx, ny = 256, 66
+    p = lio.Params(nx, ny, 3, 10, 0.1, 0.005, 1.85)
+    obst = np.zeros((ny, nx), np.uint8)
+    cells0 = np.zeros((ny, nx, 9), np.float32)
+    cells0[..., 0] = np.float32(1e-45)
+    cells0[..., 2] = np.float32(1e-40)
+    cells0[..., 4] = np.float32(-1e-40)
+    for steps in (1, 2, 3):
+        ref, _ = oracle.run(p, obst, steps, cells0)
+        assert (np.signbit(ref) & (ref == 0)).any()  # the state does produce -0.0
+        cells, _, used = gpu_run(gpu_lib, p, obst, cells0, steps, **mode_kw(gpu_lib, mode))
+        assert used == kname(mode)
+        nan_g, nan_r = np.isnan(cells), np.isnan(ref)
+        assert np.array_equal(nan_g, nan_r), f"{mode} v{version} {steps} steps: NaN positions differ"
+        same = (cells.view(np.uint32) == ref.view(np.uint32)) | nan_r
+        if not same.all():
+            bad = np.argwhere(~same)
+            y, x, k = bad[0]
+            pytest.fail(f"{mode} v{version} {steps} steps: {len(bad)} values differ, first at y={y} x={x} k={k}: "
+                        f"gpu {cells[y, x, k]!r} oracle {ref[y, x, k]!r}")
+
+
 # ------------------------------------------------ per-rank local I/O ----
 
 @pytest.mark.parametrize("parts,grid", [(1, (1, 1)), (4, (2, 2)), (3, (1, 3))])
