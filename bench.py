@@ -37,7 +37,7 @@ over ranks.  value = all cells x K / seconds / 1e6 (whole job).
 
 roofline: 72 algorithmic bytes per cell per LAUNCH (9 fp32 loads + 9 fp32
 stores; the 1-byte obstacle mask is excluded) -- a fused launch advances
-steps_per_launch time steps (the default stream kernel: 4) but moves the
+steps_per_launch time steps (the default stream kernel: 5) but moves the
 lattice through HBM once -- divided by the average launch duration measured
 with HIP events recorded by the library on the kernel's own stream over the
 timed region (device time of the K steps / launches); peak = 8000 GB/s
@@ -45,7 +45,9 @@ timed region (device time of the K steps / launches); peak = 8000 GB/s
 profiles/traffic.json (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when a
 profile of this workload + kernel exists, else null.  effective_gbs = 72 B x
 cell updates / s (SURVEY 8(d)'s MLUPS x 72 B form), which exceeds the HBM
-peak once temporal blocking pays.
+peak once temporal blocking pays.  roofline.valu = the bound that binds for
+the fused stream kernel: VALU instructions per launch and the VALU pipe's busy
+fraction from the SQ pass of the same profile (tools/pmc_traffic.py --sq).
 
 cpu_baseline: the reference's main/LbmCpu.cpp as committed (north_star: "next
 to LbmCpu.cpp timed on the same box's host cores"), built from its source by
@@ -115,17 +117,17 @@ def log(msg: str) -> None:
     print(msg, file=sys.stderr, flush=True)
 
 
-def load_traffic(workload_key: str):
-    """Per-launch HBM bytes (PMC, gfx950-corrected) from the committed profile of
-    this workload + kernel, if one was recorded (tools/pmc_traffic.py)."""
+def load_traffic(workload_key: str) -> dict:
+    """The committed PMC profile of this workload + kernel (tools/pmc_traffic.py):
+    per-launch HBM bytes (gfx950-corrected) and, from the SQ pass, the VALU
+    instructions per launch and the VALU pipe's busy fraction; {} if none."""
     f = ROOT / "profiles" / "traffic.json"
     if not f.exists():
-        return None
+        return {}
     try:
-        d = json.loads(f.read_text())
-        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+        return json.loads(f.read_text()).get(workload_key, {})
     except (ValueError, OSError):
-        return None
+        return {}
 
 
 def cpu_baseline() -> dict | None:
@@ -446,7 +448,8 @@ def main() -> int:
     achieved = BYTES_PER_UPDATE * cells_per_gpu / per_launch_s / 1e9
     effective = achieved * steps_per_launch
     wl_key = f"{tnx}x{tny}/{kernel_used}" + (str(steps_per_launch) if kernel_used == "stream" else "")
-    traffic = load_traffic(wl_key)
+    prof = load_traffic(wl_key)
+    traffic = prof.get("hbm_bytes_per_launch")
 
     out = {
         "metric": METRIC,
@@ -476,7 +479,9 @@ def main() -> int:
                      # SURVEY 8(d) form: 72 B x cell updates / s; a fused S-step launch moves
                      # the lattice through HBM once per S updates, so this can exceed the peak
                      "effective_gbs": round(effective, 1),
-                     "effective_frac": round(effective / HBM_PEAK_GBS, 4)},
+                     "effective_frac": round(effective / HBM_PEAK_GBS, 4),
+                     # the bound that binds: the VALU pipe, from the same profile
+                     "valu": prof.get("valu"), "profile": prof.get("profile")},
         "av_vels_finite": m["finite"],
     }
     aux = out.setdefault("aux", {})

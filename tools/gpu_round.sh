@@ -6,7 +6,8 @@
 #   /usr/local/graft/bin/gpurun --timeout 1500 -- bash tools/gpu_round.sh
 # then: python3 tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch/fetch_counter_collection.csv \
 #         --write gpurun_out/pmc_write/write_counter_collection.csv --kernel "stream_steps2d<5" \
-#         --key 8192x8192/stream5 --cells 67108864 --out profiles/traffic.json
+#         --sq gpurun_out/pmc_sq/sq_counter_collection.csv --key 8192x8192/stream5 --cells 67108864 \
+#         --profile "profiles/rNN/...: kernel, date" --out profiles/traffic.json
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE"

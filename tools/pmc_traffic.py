@@ -11,7 +11,13 @@ slightly over-counts those narrow reads (upper bound).
 
   python tools/pmc_traffic.py --fetch DIR/fetch_counter_collection.csv \
       --write DIR/write_counter_collection.csv --key 8192x8192/step2 --cells 67108864 \
-      --out profiles/traffic.json
+      [--sq DIR/sq_counter_collection.csv] --out profiles/traffic.json
+
+--sq adds the VALU side of the same kernel from the SQ pass (tools/gpu_round.sh):
+VALU instructions per launch and the VALU pipe's busy fraction,
+4 x SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) / (SIMDs x
+GRBM_GUI_ACTIVE / 8 XCDs) -- at two waves per SIMD only one issues VALU at a
+time, so this is the share of SIMD cycles the VALU pipe was taken.
 """
 from __future__ import annotations
 
@@ -30,6 +36,20 @@ def per_launch(path: str, counter: str, kernel_substr: str):
     return statistics.median(vals), len(vals)
 
 
+def per_dispatch(path: str, kernel_substr: str):
+    """Counter sums per dispatch (a counter may have one row per dimension), median over dispatches."""
+    by = {}
+    for r in csv.DictReader(open(path)):
+        if kernel_substr not in r["Kernel_Name"]:
+            continue
+        d = by.setdefault(r["Dispatch_Id"], {})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    if not by:
+        raise SystemExit(f"no rows for kernels matching {kernel_substr!r} in {path}")
+    keys = set().union(*by.values())
+    return {k: statistics.median(d[k] for d in by.values() if k in d) for k in keys}, len(by)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
@@ -38,6 +58,9 @@ def main():
     ap.add_argument("--key", required=True)
     ap.add_argument("--cells", type=int, required=True)
     ap.add_argument("--out", default="profiles/traffic.json")
+    ap.add_argument("--sq", default=None, help="SQ pass csv (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE)")
+    ap.add_argument("--simds", type=int, default=1024, help="SIMDs of the device (256 CUs x 4)")
+    ap.add_argument("--profile", default=None, help="where the csv files are committed (recorded in the entry)")
     a = ap.parse_args()
     fetch_kib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
     write_kib, nw = per_launch(a.write, "WRITE_SIZE", a.kernel)
@@ -53,6 +76,20 @@ def main():
         "ratio_to_algorithmic": round((read_b + write_b) / alg, 4),
         "correction": "FETCH_SIZE x2 (gfx950 wide-stream undercount), KiB x1024",
     }
+    if a.sq:
+        sq, nd = per_dispatch(a.sq, a.kernel)
+        cycles = sq["GRBM_GUI_ACTIVE"] / 8
+        entry["valu"] = {
+            "instr_per_launch": int(sq["SQ_INSTS_VALU"]),
+            "busy_frac": round(4 * sq["SQ_ACTIVE_INST_VALU"] / (a.simds * cycles), 4),
+            "clock_ghz_pmc_pass": round(cycles / (statistics.median(
+                int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(a.sq))
+                if a.kernel in r["Kernel_Name"]) * 1e-9) / 1e9, 3),
+            "dispatches": nd,
+            "def": "4 x SQ_ACTIVE_INST_VALU / (SIMDs x GRBM_GUI_ACTIVE / 8)",
+        }
+    if a.profile:
+        entry["profile"] = a.profile
     out = Path(a.out)
     d = json.loads(out.read_text()) if out.exists() else {}
     d[a.key] = entry
