@@ -326,11 +326,11 @@ __global__ __launch_bounds__(B3X * B3Y) void step3d_pair(Step3Args a, int planes
 // ---------------------------------------------------------------------------
 // Two time steps per pass over the lattice (one slab, z periodic): 2.5-D
 // temporal blocking.  A block of 64 columns (one wave, one column per lane) x
-// T3H rows (one wave per row) walks a segment of z planes; as input plane j
+// TH rows (one wave per row) walks a segment of z planes; as input plane j
 // arrives (step t, 19 coalesced loads per lane), level 1 computes plane j-1 at
 // t+1 and level 2 computes plane j-2 at t+2 from level 1's planes, so the
 // lattice crosses HBM once per two steps.  Owned outputs: the inner 60 x
-// (T3H - 4) cells (a two-cell ring in x and y is recomputed).
+// (TH - 4) cells (a two-cell ring in x and y is recomputed).
 // Pulls, per level, for the centre plane z (input plane z+1 just arrived):
 //   own row, x +- 1 by DPP:   speeds 0,1,2 of plane z, 9,10,11 of plane z-1
 //                             (registers kept from earlier iterations),
@@ -343,10 +343,21 @@ __global__ __launch_bounds__(B3X * B3Y) void step3d_pair(Step3Args a, int planes
 // stores) x 4 B / 2 = 99 B instead of 152.  Same cell3d arithmetic: bitwise
 // equal to the one-step kernels.
 // ---------------------------------------------------------------------------
-constexpr int T3W = 64, T3H = 12;
-constexpr int T3OX = T3W - 4, T3OY = T3H - 4;
-constexpr int T3C = T3W * T3H;               // cells per plane slot
-constexpr int T3LDS = (2 + 2 * 6 + 3 * 2) * T3C;  // floats per level: M, Z[2][6], P[3][2]
+// TH = rows per block (waves), a template parameter (LBM3D_TH): two levels of
+// 20 plane slots of 64 x TH floats take 10 x TH KB of LDS (TH <= 15).
+// SKIP: a wave whose row no level-2 (level-1) cell depends on skips that
+// level's collision (rows 0 and TH-1 at level 1; rows 0, 1, TH-2, TH-1 at
+// level 2) -- it still writes and reads its LDS slots and barriers, and the
+// skipped values are never read (level 2 of rows 2 .. TH-3 pulls from level-1
+// rows 1 .. TH-2).
+constexpr int T3W = 64;
+constexpr int T3OX = T3W - 4;  // owned columns
+template <int TH>
+struct T3 {
+    static constexpr int C = T3W * TH;                    // cells per plane slot
+    static constexpr int LDS = (2 + 2 * 6 + 3 * 2) * C;   // floats per level: M, Z[2][6], P[3][2]
+    static constexpr int OY = TH - 4;                     // owned rows
+};
 
 struct Two3Args {
     const float *fin;   // origin of the lattice read (ghost planes -2, -1, nz, nz + 1 filled)
@@ -361,10 +372,13 @@ struct Two3Args {
 };
 
 // One level for centre plane jz - 1, input plane jz (in).  Must be reached by
-// every thread of the block (it holds a barrier).
+// every thread of the block (it holds a barrier).  live (wave-uniform): some
+// later level or output needs this row's result.
+template <int TH>
 __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3], float *lds, int jz, float (&r0)[3],
-                                        float (&r9a)[3], float (&r9b)[3], int lane, int wy, bool ob,
+                                        float (&r9a)[3], float (&r9b)[3], int lane, int wy, bool ob, bool live,
                                         const Two3Args &a) {
+    constexpr int T3C = T3<TH>::C;
     float *M = lds, *Z = lds + 2 * T3C, *P = lds + 14 * T3C;
     const int c = wy * T3W + lane;
     const int zw = jz & 1, pw = ((jz % 3) + 3) % 3;  // slots of plane jz
@@ -375,7 +389,7 @@ __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3],
     P[(pw * 2) * T3C + c] = in[12];
     P[(pw * 2 + 1) * T3C + c] = in[13];
     __syncthreads();
-    const int wm = max(wy - 1, 0) * T3W, wp = min(wy + 1, T3H - 1) * T3W;
+    const int wm = max(wy - 1, 0) * T3W, wp = min(wy + 1, TH - 1) * T3W;
     const int lm = max(lane - 1, 0), lp = min(lane + 1, T3W - 1);
     const float *z = Z + ((jz - 1) & 1) * 6 * T3C;          // plane jz - 1
     const float *p = P + ((((jz - 2) % 3) + 3) % 3) * 2 * T3C;  // plane jz - 2
@@ -399,7 +413,13 @@ __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3],
     s[16] = dpp_from_left(in[16]);
     s[17] = M[wp + lane];
     s[18] = M[T3C + wm + lane];
-    const float u = cell3d(s, out, ob, a.omega, a.omo, a.w1, a.w2);
+    float u = 0.f;
+    if (live) {
+        u = cell3d(s, out, ob, a.omega, a.omo, a.w1, a.w2);
+    } else {
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) out[k] = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         r9b[i] = r9a[i];
@@ -409,14 +429,18 @@ __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3],
     return u;
 }
 
-__global__ __launch_bounds__(T3W * T3H) void step3d_two(Two3Args a) {
-    __shared__ float lds1[T3LDS], lds2[T3LDS];
-    __shared__ float red[2][T3H];
-    const int lane = threadIdx.x, wy = threadIdx.y;
-    const int ox = blockIdx.x * T3OX, oy = blockIdx.y * T3OY;
+// PD: input planes in flight -- 1: plane j+1 while j is computed; 2: also j+2
+// (19 more VGPRs; one 768..960-thread block per CU keeps few loads in flight).
+template <int TH, bool SKIP, int PD>
+__global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
+    __shared__ float lds1[T3<TH>::LDS], lds2[T3<TH>::LDS];
+    __shared__ float red[2][TH];
+    const int lane = threadIdx.x, wy = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int ox = blockIdx.x * T3OX, oy = blockIdx.y * T3<TH>::OY;
+    const bool live1 = !SKIP || (wy >= 1 && wy < TH - 1), live2 = !SKIP || (wy >= 2 && wy < TH - 2);
     const int x = (((ox - 2 + lane) % a.nx) + a.nx) % a.nx;
     const int y = (((oy - 2 + wy) % a.ny) + a.ny) % a.ny;
-    const bool own = lane >= 2 && lane < T3W - 2 && wy >= 2 && wy < T3H - 2 && ox + lane - 2 < a.nx &&
+    const bool own = lane >= 2 && lane < T3W - 2 && wy >= 2 && wy < TH - 2 && ox + lane - 2 < a.nx &&
                      oy + wy - 2 < a.ny;
     const int zs = a.z0 + blockIdx.z * a.seg, ze = min(zs + a.seg, a.zn);
     const long long row = (long long)y * a.px + x;
@@ -427,26 +451,38 @@ __global__ __launch_bounds__(T3W * T3H) void step3d_two(Two3Args a) {
         zz = min(max(zz, -2), a.nz + 1);
         return a.obst[((long long)zz * a.ny + y) * a.nx + x] != 0;
     };
-    // input planes are prefetched one iteration ahead (their loads stay in
+    // input planes are prefetched PD iterations ahead (their loads stay in
     // flight across the two barriers of the current iteration)
-    float in[Q3];
+    float in[Q3], far[Q3];
     bool ob1 = obz(zs - 3), ob2 = obz(zs - 4);
     {
         const float *pl = a.fin + (long long)(zs - 2) * a.PL + row;
 #pragma unroll
         for (int k = 0; k < Q3; ++k) in[k] = pl[k * a.KS];
+        if (PD == 2) {
+            const float *pf = a.fin + (long long)min(zs - 1, ze + 1) * a.PL + row;
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) far[k] = pf[k * a.KS];
+        }
     }
     for (int j = zs - 2; j <= ze + 1; ++j) {
         float nin[Q3];
-        const float *pn = a.fin + (long long)min(j + 1, ze + 1) * a.PL + row;
+        const float *pn = a.fin + (long long)min(j + PD, ze + 1) * a.PL + row;
+        if (PD == 2) {
 #pragma unroll
-        for (int k = 0; k < Q3; ++k) nin[k] = pn[k * a.KS];
+            for (int k = 0; k < Q3; ++k) nin[k] = far[k];
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) far[k] = pn[k * a.KS];
+        } else {
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) nin[k] = pn[k * a.KS];
+        }
         ob2 = ob1;
         ob1 = obz(j - 1);
         float o1[Q3], o2[Q3];
-        const float v1 = level3(in, o1, lds1, j, r0a, r9aa, r9ba, lane, wy, ob1, a);
+        const float v1 = level3<TH>(in, o1, lds1, j, r0a, r9aa, r9ba, lane, wy, ob1, live1, a);
         if (own && j - 1 >= zs && j - 1 < ze) u1 += v1;
-        const float v2 = level3(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, lane, wy, ob2, a);
+        const float v2 = level3<TH>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, lane, wy, ob2, live2, a);
         if (own && j - 2 >= zs && j - 2 < ze) {
             u2 += v2;
             float *d = a.fout + (long long)(j - 2) * a.PL + row;
@@ -469,7 +505,7 @@ __global__ __launch_bounds__(T3W * T3H) void step3d_two(Two3Args a) {
     if (lane == 0 && wy == 0) {
         float b1 = red[0][0], b2 = red[1][0];
 #pragma unroll
-        for (int i = 1; i < T3H; ++i) {
+        for (int i = 1; i < TH; ++i) {
             b1 += red[0][i];
             b2 += red[1][i];
         }
@@ -577,6 +613,9 @@ struct lbm3d_handle {
     bool nt = true;    // LBM3D_NT: non-temporal output stores
     bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two), single slab or z slabs
     int seg = 64;      // LBM3D_SEG: z planes per block of the two-step kernel (32-128 equal within noise at 512^3)
+    int th = 12;       // LBM3D_TH: rows (waves) per block of the two-step kernel (12, 14, 15)
+    bool skip = false; // LBM3D_SKIP: waves skip the collisions of rows no later level reads (not faster)
+    int pd = 1;        // LBM3D_PD: input planes in flight in the two-step kernel (1, 2)
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
     ncclComm_t comm = nullptr;
@@ -614,6 +653,9 @@ struct lbm3d_handle {
         if (const char *n = getenv("LBM3D_NT")) nt = atoi(n) != 0;
         if (const char *t = getenv("LBM3D_TWO")) two = atoi(t) != 0;
         if (const char *g = getenv("LBM3D_SEG")) seg = std::max(1, atoi(g));
+        if (const char *h = getenv("LBM3D_TH")) th = (atoi(h) == 14 || atoi(h) == 15) ? atoi(h) : 12;
+        if (const char *k = getenv("LBM3D_SKIP")) skip = atoi(k) != 0;
+        if (const char *d = getenv("LBM3D_PD")) pd = atoi(d) == 2 ? 2 : 1;
         KS = (long long)p.ny * px;
         PL = (long long)Q3 * KS;
         // round-robin z extents (StructuredGridUtils.hpp:161-165 rule, in z)
@@ -724,7 +766,7 @@ struct lbm3d_handle {
         return r;
     }
     int two_blocks(int z0, int zn) const {
-        return ((p.nx + T3OX - 1) / T3OX) * ((p.ny + T3OY - 1) / T3OY) * ((zn - z0 + seg - 1) / seg);
+        return ((p.nx + T3OX - 1) / T3OX) * ((p.ny + th - 5) / (th - 4)) * ((zn - z0 + seg - 1) / seg);
     }
     // two-step passes: one slab, or z slabs of at least 4 planes (ghosts are 2 planes of the neighbours)
     bool use_two() const {
@@ -757,8 +799,21 @@ struct lbm3d_handle {
         a.partials = s.partials2;
         a.nblocks = s.nblk_two;
         a.blk0 = blk0;
-        const dim3 g((p.nx + T3OX - 1) / T3OX, (p.ny + T3OY - 1) / T3OY, (zn - z0 + seg - 1) / seg);
-        hipLaunchKernelGGL(step3d_two, g, dim3(T3W, T3H), 0, st, a);
+        const dim3 g((p.nx + T3OX - 1) / T3OX, (p.ny + th - 5) / (th - 4), (zn - z0 + seg - 1) / seg);
+        const dim3 b(T3W, th);
+        switch ((th * 2 + (skip ? 1 : 0)) * 2 + (pd - 1)) {
+            case 48: hipLaunchKernelGGL((step3d_two<12, false, 1>), g, b, 0, st, a); break;
+            case 49: hipLaunchKernelGGL((step3d_two<12, false, 2>), g, b, 0, st, a); break;
+            case 50: hipLaunchKernelGGL((step3d_two<12, true, 1>), g, b, 0, st, a); break;
+            case 51: hipLaunchKernelGGL((step3d_two<12, true, 2>), g, b, 0, st, a); break;
+            case 56: hipLaunchKernelGGL((step3d_two<14, false, 1>), g, b, 0, st, a); break;
+            case 58: hipLaunchKernelGGL((step3d_two<14, true, 1>), g, b, 0, st, a); break;
+            case 59: hipLaunchKernelGGL((step3d_two<14, true, 2>), g, b, 0, st, a); break;
+            case 60: hipLaunchKernelGGL((step3d_two<15, false, 1>), g, b, 0, st, a); break;
+            case 62: hipLaunchKernelGGL((step3d_two<15, true, 1>), g, b, 0, st, a); break;
+            case 63: hipLaunchKernelGGL((step3d_two<15, true, 2>), g, b, 0, st, a); break;
+            default: hipLaunchKernelGGL((step3d_two<12, true, 1>), g, b, 0, st, a); break;
+        }
         H3(hipGetLastError());
     }
 

@@ -235,3 +235,24 @@ def test_d3q19_rccl_two_step_self_exchange_bitwise(gpu_lib):
                            devices=[0], unique_id=gpu_lib.rccl_unique_id())
         assert np.array_equal(cells, ref)
         np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("th,skip,pd", [("12", "0", "1"), ("12", "1", "1"), ("14", "1", "1"), ("15", "1", "1"), ("15", "0", "1"),
+                                         ("12", "1", "2"), ("15", "1", "2")])
+@pytest.mark.parametrize("nx,ny,nz,parts", [(64, 8, 5, 1), (125, 23, 9, 1), (61, 17, 3, 1), (70, 31, 24, 3)])
+def test_d3q19_two_step_block_rows_bitwise(gpu_lib, nx, ny, nz, parts, th, skip, pd, monkeypatch):
+    """The two-step kernel's block heights (LBM3D_TH: 12, 14, 15 rows = waves,
+    up to 150 KB of LDS) with and without the wave-uniform skip of the rows no
+    later level reads (LBM3D_SKIP): bitwise vs the oracle on partial and
+    wrapped tiles (ny below and above one block's owned rows), one slab and
+    z slabs, 9 steps (four passes + one one-step launch)."""
+    monkeypatch.setenv("LBM3D_TH", th)
+    monkeypatch.setenv("LBM3D_SKIP", skip)
+    monkeypatch.setenv("LBM3D_PD", pd)
+    monkeypatch.setenv("LBM3D_SEG", "4")
+    p, obst, c0 = _problem(nx, ny, nz, nx * ny + nz)
+    ref, ref_av = oracle.run3d(p, obst, 9, c0)
+    cells, av = _gpu3d(gpu_lib, p, obst, c0, 9, parts=parts, devices=[0])
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
