@@ -1,0 +1,43 @@
+"""bench.py's output contract on one GPU (the line the driver parses).
+
+Runs `python bench.py` in a subprocess with a short step count and checks the
+one JSON line: the keys and types the driver reads, the roofline and
+cpu_baseline objects' shape, and that value / ms_per_step agree.
+"""
+from __future__ import annotations
+
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+pytestmark = pytest.mark.gpu
+
+
+def run_bench(*args):
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], cwd=ROOT, capture_output=True, text=True,
+                         timeout=240, check=True)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_json_contract():
+    d = run_bench("--steps", "10", "--warmup", "2", "--no-cpu-baseline", "--no-aux")
+    for k, t in (("metric", str), ("value", float), ("unit", str), ("n_gpus", int), ("steps", int), ("warmup", int),
+                 ("ms_per_step", float), ("higher_is_better", bool), ("scaling", str), ("dtype", str), ("data", str),
+                 ("config", dict), ("roofline", dict)):
+        assert isinstance(d[k], t), k
+    assert d["n_gpus"] == 1 and d["steps"] == 10 and d["warmup"] == 2
+    assert d["unit"] == "MLUPS" and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert "vs_baseline" in d and d["vs_baseline"] is None
+    assert "workload" in d["config"] and "8192x8192" in d["config"]["workload"]
+    r = d["roofline"]
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert 0 < r["frac"] < 1 and r["achieved"] == pytest.approx(r["frac"] * r["peak"], rel=1e-3)
+    # value (whole-job MLUPS) and ms_per_step describe the same timed region
+    assert d["value"] == pytest.approx(8192 * 8192 / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
+    assert d["av_vels_finite"] is True
