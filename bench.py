@@ -68,6 +68,7 @@ import os
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 from pathlib import Path
 
@@ -394,6 +395,47 @@ def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: 
         eng.close()
 
 
+class AuxWatchdog:
+    """Bounds the aux phase.  The main measurement is done when it starts; an aux
+    that hangs (e.g. one rank failed an aux and left the others waiting in an
+    RCCL exchange) would otherwise keep rank 0 from ever printing the line.  Past
+    the budget, rank 0 prints the line with the aux finished so far plus a note,
+    and every rank exits (so the launcher's other ranks end too)."""
+
+    def __init__(self, budget_s: float, out: dict, rank: int):
+        self.out, self.rank = out, rank
+        self.lock = threading.Lock()
+        self.printed = False
+        self.timer = None
+        if budget_s > 0:
+            self.timer = threading.Timer(budget_s, self._fire, args=(budget_s,))
+            self.timer.daemon = True
+            self.timer.start()
+
+    def _print(self, out: dict) -> None:
+        with self.lock:
+            if self.printed:
+                return
+            self.printed = True
+            if self.rank == 0:
+                print(json.dumps(out), flush=True)
+
+    def _fire(self, budget_s: float) -> None:
+        try:
+            out = json.loads(json.dumps(self.out))  # a consistent copy
+        except (TypeError, ValueError, RuntimeError):
+            out = {k: v for k, v in self.out.items() if k != "aux"}
+        out.setdefault("aux", {})["watchdog"] = f"aux phase exceeded {budget_s:.0f} s; the remaining aux were skipped"
+        self._print(out)
+        log(f"aux watchdog: {budget_s:.0f} s exceeded, exiting")
+        os._exit(0)
+
+    def finish(self) -> None:
+        if self.timer is not None:
+            self.timer.cancel()
+        self._print(self.out)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -411,6 +453,9 @@ def main() -> int:
     ap.add_argument("--no-d3q19", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="skip the 16384^2 strong-scaling aux (config 4)")
     ap.add_argument("--d3q19-n", type=int, default=512, help="D3Q19 aux grid edge (BASELINE config 5: 512)")
+    ap.add_argument("--aux-budget", type=float, default=300.0,
+                    help="seconds the aux measurements may take after the main one; past it rank 0 prints the "
+                         "line with the aux done so far and every rank exits (0: no limit)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -485,6 +530,7 @@ def main() -> int:
         "av_vels_finite": m["finite"],
     }
     aux = out.setdefault("aux", {})
+    watchdog = AuxWatchdog(args.aux_budget, out, rank)
     if n > 1 and not args.no_aux:
         try:
             ms = measure_weak(tnx, tny, n, 1, args, kernel, kflags, rank, world, local_rank, dist_on)
@@ -527,8 +573,7 @@ def main() -> int:
                     aux[key] = r
     if not aux:
         out.pop("aux")
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    watchdog.finish()
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
