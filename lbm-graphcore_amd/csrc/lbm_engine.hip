@@ -199,7 +199,7 @@ struct lbm_handle {
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     int stream_waves = 2;    // LBM_STREAM_W: register target of the two-column kernel (waves per SIMD)
     int stream_cfg = 0;      // LBM_STREAM_CFG (v3): 0 one wave per workgroup; 1 four waves (adjacent strips);
-                             // 2 four waves + non-temporal lattice stores
+                             // 2 four waves + non-temporal lattice stores; 3 one wave + non-temporal stores
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
@@ -262,7 +262,7 @@ struct lbm_handle {
         stream_hs = std::max(0, env_int("LBM_STREAM_HS", stream_hs));
         stream_v = std::min(std::max(env_int("LBM_STREAM_V", stream_v), 1), 3);
         stream_waves = env_int("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
-        stream_cfg = std::min(std::max(env_int("LBM_STREAM_CFG", stream_cfg), 0), 2);
+        stream_cfg = std::min(std::max(env_int("LBM_STREAM_CFG", stream_cfg), 0), 3);
         stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
             const char *g = getenv("LBM_STREAM_GUIDE");
@@ -605,7 +605,7 @@ struct lbm_handle {
             if (!(so && atoi(so) == 0)) {
                 std::vector<uint8_t> fl((size_t)ni + nb);
                 HIP_CHECK(hipMemcpy(fl.data(), s.uobst, fl.size(), hipMemcpyDeviceToHost));
-                const int W = stream_cfg == 0 ? 1 : 4;
+                const int W = (stream_cfg == 0 || stream_cfg == 3) ? 1 : 4;
                 std::vector<int> perm((size_t)ni + nb);
                 auto order = [&](int off, int n) {
                     const int blocks = (n + W - 1) / W, q = blocks / 8, r = blocks % 8;
@@ -888,6 +888,16 @@ struct lbm_handle {
                             (void)hipGetLastError();
                         }
                     }
+        }
+        // v3 launch form by sub-domain size unless LBM_STREAM_CFG says otherwise:
+        // non-temporal lattice stores (cfg 3) from 2^27 cells up -- 16384^2: 287 vs
+        // 259 GLUPS; 8192^2 equal; 4096^2 -5 % (its lattice pair stays in the
+        // 256 MB infinity cache between launches only without them)
+        // (profiles/r02/ab_nt_stores.log)
+        if (!getenv("LBM_STREAM_CFG")) {
+            long long big = 0;
+            for (const auto &s : subs) big = std::max(big, (long long)s.w * s.h);
+            stream_cfg = big >= (1LL << 27) ? 3 : 0;
         }
         for (auto &s : subs) {
             set_device(s);

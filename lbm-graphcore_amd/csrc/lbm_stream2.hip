@@ -524,7 +524,7 @@ static void launch_s2d(const StreamArgs &a, int units, bool reduce, hipStream_t 
 }
 
 // waves per CU of the configuration (cfg: 0 = one wave per workgroup, plain
-// stores; 1 = four waves, plain; 2 = four waves, nt stores)
+// stores; 1 = four waves, plain; 2 = four waves, nt stores; 3 = one wave, nt stores)
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n) {
     const void *fn = steps == 2   ? (const void *)&stream_steps2d<2, false, 1, false>
                      : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false>
@@ -549,6 +549,11 @@ hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduc
         case 50: launch_s2d<5, 1, false>(a, units, reduce, s); break;
         case 51: launch_s2d<5, 4, false>(a, units, reduce, s); break;
         case 52: launch_s2d<5, 4, true>(a, units, reduce, s); break;
+        case 23: launch_s2d<2, 1, true>(a, units, reduce, s); break;
+        case 33: launch_s2d<3, 1, true>(a, units, reduce, s); break;
+        case 43: launch_s2d<4, 1, true>(a, units, reduce, s); break;
+        case 53: launch_s2d<5, 1, true>(a, units, reduce, s); break;
+        case 63: launch_s2d<6, 1, true>(a, units, reduce, s); break;
         case 60: launch_s2d<6, 1, false>(a, units, reduce, s); break;
         case 61: launch_s2d<6, 4, false>(a, units, reduce, s); break;
         case 62: launch_s2d<6, 4, true>(a, units, reduce, s); break;
