@@ -585,6 +585,7 @@ struct fail3 : std::runtime_error {
 struct Slab {
     int id = 0, dev = 0, z0 = 0, nzs = 0;
     float *f[2] = {nullptr, nullptr};  // allocations (ghost plane below first)
+    bool f_joint = false;              // f[1] lies in f[0]'s allocation (LBM_LATTICE_PAD)
     float *o[2] = {nullptr, nullptr};  // origins: plane z = 0
     uint8_t *obst = nullptr;
     uint8_t *obst_g = nullptr;   // [nzs + 4][ny][nx]: obst with two image planes each side (two-step kernel)
@@ -616,6 +617,7 @@ struct lbm3d_handle {
     int th = 12;       // LBM3D_TH: rows (waves) per block of the two-step kernel (12, 14, 15)
     bool skip = false; // LBM3D_SKIP: waves skip the collisions of rows no later level reads (not faster)
     int pd = 1;        // LBM3D_PD: input planes in flight in the two-step kernel (1, 2)
+    long long kspad = 0;  // LBM3D_KSPAD: floats appended to each speed plane (multiple of 64)
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
     ncclComm_t comm = nullptr;
@@ -656,7 +658,8 @@ struct lbm3d_handle {
         if (const char *h = getenv("LBM3D_TH")) th = (atoi(h) == 14 || atoi(h) == 15) ? atoi(h) : 12;
         if (const char *k = getenv("LBM3D_SKIP")) skip = atoi(k) != 0;
         if (const char *d = getenv("LBM3D_PD")) pd = atoi(d) == 2 ? 2 : 1;
-        KS = (long long)p.ny * px;
+        if (const char *k = getenv("LBM3D_KSPAD")) kspad = (std::max(0LL, atoll(k)) + 63) / 64 * 64;
+        KS = (long long)p.ny * px + kspad;
         PL = (long long)Q3 * KS;
         // round-robin z extents (StructuredGridUtils.hpp:161-165 rule, in z)
         all_z0.assign(parts, 0);
@@ -724,11 +727,23 @@ struct lbm3d_handle {
         H3(hipSetDevice(s.dev));
         // two ghost planes below and above (the two-step kernel reads both)
         const size_t floats = (size_t)(s.nzs + 4) * PL;
-        for (int k = 0; k < 2; ++k) {
-            H3(hipMalloc(&s.f[k], floats * sizeof(float)));
-            H3(hipMemset(s.f[k], 0, floats * sizeof(float)));
-            s.o[k] = s.f[k] + 2 * PL;
+        const char *lp = getenv("LBM_LATTICE_PAD");
+        if (lp && *lp) {
+            // both lattices in one allocation, the second pad bytes (rounded to
+            // 256 B) after the end of the first (see lbm_engine.hip alloc_sub)
+            const size_t second = floats + (size_t)(std::max(0LL, atoll(lp)) + 255) / 256 * 64;
+            const size_t n = (second + floats) * sizeof(float);
+            H3(hipMalloc(&s.f[0], n));
+            H3(hipMemset(s.f[0], 0, n));
+            s.f[1] = s.f[0] + second;
+            s.f_joint = true;
+        } else {
+            for (int k = 0; k < 2; ++k) {
+                H3(hipMalloc(&s.f[k], floats * sizeof(float)));
+                H3(hipMemset(s.f[k], 0, floats * sizeof(float)));
+            }
         }
+        for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + 2 * PL;
         const size_t ob = (size_t)s.nzs * p.ny * p.nx, plane = (size_t)p.ny * p.nx;
         H3(hipMalloc(&s.obst, ob + 256));
         H3(hipMemcpy(s.obst, obstacles + (size_t)s.z0 * plane, ob, hipMemcpyHostToDevice));
@@ -1218,7 +1233,7 @@ struct lbm3d_handle {
             if (hipSetDevice(s.dev) != hipSuccess) continue;
             (void)hipDeviceSynchronize();
             for (int k = 0; k < 2; ++k)
-                if (s.f[k]) (void)hipFree(s.f[k]);
+                if (s.f[k] && !(k == 1 && s.f_joint)) (void)hipFree(s.f[k]);
             if (s.obst) (void)hipFree(s.obst);
             if (s.obst_g) (void)hipFree(s.obst_g);
             if (s.partials) (void)hipFree(s.partials);

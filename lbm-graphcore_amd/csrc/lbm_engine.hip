@@ -145,6 +145,7 @@ struct Sub {
     long long plane = 0;
     long long lattice_floats = 0, origin_off = 0;
     float *f[2] = {nullptr, nullptr};   // allocations
+    bool f_joint = false;                // f[1] lies in f[0]'s allocation (LBM_LATTICE_PAD)
     float *o[2] = {nullptr, nullptr};   // origins: cell (0,0), plane 0
     uint8_t *obst = nullptr;            // [h][w]
     uint8_t *obst_g = nullptr;          // [(h+2og)][(w+2og)], periodic / neighbour images in the ring
@@ -889,16 +890,6 @@ struct lbm_handle {
                         }
                     }
         }
-        // v3 launch form by sub-domain size unless LBM_STREAM_CFG says otherwise:
-        // non-temporal lattice stores (cfg 3) from 2^27 cells up -- 16384^2: 287 vs
-        // 259 GLUPS; 8192^2 equal; 4096^2 -5 % (its lattice pair stays in the
-        // 256 MB infinity cache between launches only without them)
-        // (profiles/r02/ab_nt_stores.log)
-        if (!getenv("LBM_STREAM_CFG")) {
-            long long big = 0;
-            for (const auto &s : subs) big = std::max(big, (long long)s.w * s.h);
-            stream_cfg = big >= (1LL << 27) ? 3 : 0;
-        }
         for (auto &s : subs) {
             set_device(s);
             build_args(s);
@@ -1174,11 +1165,23 @@ struct lbm_handle {
             s.lattice_floats = Q * s.plane;
         }
         s.origin_off = (long long)gr * s.pitch + xoff;
-        for (int k = 0; k < 2; ++k) {
-            HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)s.lattice_floats));
-            HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)s.lattice_floats));
-            s.o[k] = s.f[k] + s.origin_off;
+        const char *lp = getenv("LBM_LATTICE_PAD");
+        if (lp && *lp) {
+            // both lattices in one allocation, the second pad bytes (rounded to
+            // 256 B) after the end of the first
+            const long long second = s.lattice_floats + (std::max(0LL, atoll(lp)) + 255) / 256 * 64;
+            const size_t n = sizeof(float) * (size_t)(second + s.lattice_floats);
+            HIP_CHECK(hipMalloc(&s.f[0], n));
+            HIP_CHECK(hipMemset(s.f[0], 0, n));
+            s.f[1] = s.f[0] + second;
+            s.f_joint = true;
+        } else {
+            for (int k = 0; k < 2; ++k) {
+                HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)s.lattice_floats));
+                HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)s.lattice_floats));
+            }
         }
+        for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + s.origin_off;
         HIP_CHECK(hipMalloc(&s.obst, (size_t)round_up((long long)s.w * s.h + 16, 256)));
         HIP_CHECK(hipMemcpy2D(s.obst, (size_t)s.w, obstacles + (size_t)s.rect.y0 * p.nx + s.rect.x0, (size_t)p.nx,
                               (size_t)s.w, (size_t)s.h, hipMemcpyHostToDevice));
@@ -1631,7 +1634,7 @@ struct lbm_handle {
             if (hipSetDevice(s.dev) != hipSuccess) continue;
             (void)hipDeviceSynchronize();
             for (int k = 0; k < 2; ++k) {
-                if (s.f[k]) (void)hipFree(s.f[k]);
+                if (s.f[k] && !(k == 1 && s.f_joint)) (void)hipFree(s.f[k]);
                 if (s.partials[k]) (void)hipFree(s.partials[k]);
             }
             if (s.obst) (void)hipFree(s.obst);

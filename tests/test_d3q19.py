@@ -256,3 +256,23 @@ def test_d3q19_two_step_block_rows_bitwise(gpu_lib, nx, ny, nz, parts, th, skip,
     cells, av = _gpu3d(gpu_lib, p, obst, c0, 9, parts=parts, devices=[0])
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"LBM3D_KSPAD": "320"}, {"LBM_LATTICE_PAD": "4096"},
+                                 {"LBM_LATTICE_PAD": "1052672", "LBM3D_KSPAD": "64"}])
+@pytest.mark.parametrize("two", ["0", "1"])
+@pytest.mark.parametrize("nx,ny,nz,parts", [(64, 8, 5, 1), (70, 31, 24, 3)])
+def test_d3q19_lattice_placement_bitwise(gpu_lib, nx, ny, nz, parts, two, env, monkeypatch):
+    """Lattice placement knobs (padded speed planes, both
+    lattices in one allocation): bitwise vs the oracle with
+    the one- and two-step kernels, one slab and z slabs."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("LBM3D_TWO", two)
+    p, obst, c0 = _problem(nx, ny, nz, nx + ny * nz)
+    ref, ref_av = oracle.run3d(p, obst, 7, c0)
+    cells, av = _gpu3d(gpu_lib, p, obst, c0, 7, parts=parts, devices=[0])
+    bad = np.argwhere(cells != ref)
+    assert len(bad) == 0, (len(bad), bad[:8].tolist(), sorted(set(bad[:, 0].tolist())), sorted(set(bad[:, 3].tolist())))
+    np.testing.assert_allclose(av, ref_av, rtol=1e-5)

@@ -667,3 +667,22 @@ def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, S, monkeypatch):
             assert used == "stream"
             assert np.array_equal(cells, ref), (steps, kw)
             np.testing.assert_allclose(av, ref_av, rtol=5e-5)  # summation order: 78K-cell fp32 sums (seed 3: 1.2e-5)
+
+
+@pytest.mark.parametrize("env", [{"LBM_LATTICE_PAD": "4096"}, {"LBM_LATTICE_PAD": "0"}, {"LBM_LATTICE_PAD": "1052672"}])
+def test_lattice_placement_knobs_bitwise(gpu_lib, env, monkeypatch):
+    """Lattice placement knobs (both lattices in one
+    allocation at a chosen offset): bitwise vs the oracle with the v3 stream kernel on one domain and 2x2 loop-back."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("LBM_STREAM_GUIDE", "24:0.6,8:0.3,3")
+    rng = np.random.default_rng(11)
+    p = lio.Params(300, 260, 9, 10, 0.1, 0.02, 1.7)
+    obst = (rng.random((260, 300)) < 0.03).astype(np.uint8)
+    cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((260, 300, 9)))).astype(np.float32)
+    ref, ref_av = oracle.run(p, obst, 11, cells0)
+    for kw in (dict(), dict(parts=4, grid=(2, 2))):
+        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 11, devices=[0], kernel=gpu_lib.KERNEL_STREAM, **kw)
+        assert used == "stream"
+        assert np.array_equal(cells, ref), kw
+        np.testing.assert_allclose(av, ref_av, rtol=5e-5)
