@@ -35,6 +35,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "lbm_hip.h"
@@ -224,6 +225,8 @@ struct lbm_handle {
     bool force_exchange = false;
     int graph_steps = 8;     // replay graphs of 2*graph_steps launches on the single-domain path
     hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
+    std::vector<float> probe_ms;  // placement probe: ms per launch of each lattice pair tried
+    int probe_kept = -1;          // the pair kept (-1: no probe)
     // Tuning knobs (environment, read at create): LBM_TWO_STEP, LBM_MAX_BLOCKS,
     // LBM_LAYOUT (rows|planar), LBM_GRAPH_STEPS, LBM_FORCE_EXCHANGE.  Defaults
     // chosen with tools/ab_bench.py on MI355X (profiles/r01/ab_*.log).
@@ -894,6 +897,7 @@ struct lbm_handle {
             set_device(s);
             build_args(s);
         }
+        placement_probe(subs[0]);
         if (pipeline)
             for (auto &s : subs) {
                 set_device(s);
@@ -1288,6 +1292,92 @@ struct lbm_handle {
             HIP_CHECK(launch_halo_unpack(halo_args(s, target[k], mode, true), s.s_comm));
             HIP_CHECK(hipEventRecord(s.ev_u, s.s_comm));
         }
+    }
+
+    // Point the v3 stream arguments of s at lattices f0 / f1 (placement probe).
+    void set_stream_lattices(Sub &s, float *f0, float *f1) {
+        s.f[0] = f0;
+        s.f[1] = f1;
+        for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + s.origin_off;
+        for (int par = 0; par < 2; ++par) {
+            for (StreamArgs *a : {&s.a3_int[par], &s.a3_bnd[par]}) {
+                a->fin = s.o[par];
+                a->fout = s.o[1 - par];
+                for (int d = 0; d < 8; ++d) a->dst[d] = make_dst2(s, s.o[1 - par], d);
+            }
+            HIP_CHECK(hipMemcpy(s.dst2_dev + 8 * par, s.a3_int[par].dst, sizeof(Dst2) * 8, hipMemcpyHostToDevice));
+        }
+    }
+
+    // Placement probe.  The stream kernel runs a large
+    // sub-domain at one of two speed levels (about 7 % apart) set by the
+    // physical pages under its lattices, fixed for the engine's life.  A single
+    // sub-domain of at least 2^25 cells allocates LBM_PLACEMENT_TRIES (5; at most
+    // 48 GB of them) lattice pairs, all held at once, times the interior launch on each
+    // (non-reducing form: av_local and the reduction control block are not
+    // touched; constant populations; two interleaved rounds after a clock
+    // warm-up, minimum per pair), keeps the fastest pair and frees the others.  The kept
+    // pair is zeroed and the launch arguments are rebuilt, so the engine state
+    // is as if the probe had not run.  LBM_PLACEMENT_TRIES=1 turns it off.
+    void placement_probe(Sub &s) {
+        const size_t pair_bytes = 2 * sizeof(float) * (size_t)s.lattice_floats;
+        const int cap = (int)std::max<size_t>(1, (48ull << 30) / pair_bytes);  // at most 48 GB of candidates
+        const int tries = std::min({std::max(env_int("LBM_PLACEMENT_TRIES", 5), 1), 8, cap});
+        if (tries <= 1 || !use_stream || stream_v != 3 || subs.size() != 1 || multi() || s.f_joint ||
+            (long long)s.w * s.h < (1LL << 25) || s.n3_int <= 0)
+            return;
+        const size_t n = (size_t)s.lattice_floats;
+        std::vector<std::array<float *, 2>> cand{{s.f[0], s.f[1]}};
+        for (int c = 1; c < tries; ++c) {
+            std::array<float *, 2> f{nullptr, nullptr};
+            if (hipMalloc(&f[0], sizeof(float) * n) != hipSuccess) { (void)hipGetLastError(); break; }
+            if (hipMalloc(&f[1], sizeof(float) * n) != hipSuccess) {
+                (void)hipGetLastError();
+                (void)hipFree(f[0]);
+                break;
+            }
+            cand.push_back(f);
+        }
+        const unsigned fill = 0x3dcccccdu;  // 0.1f: rho = 0.9 everywhere, no tiny-density path
+        for (auto &f : cand)
+            for (float *p : f) HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), (int)fill, n, s.s_comp));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        std::vector<float> best(cand.size(), 1e30f);
+        const int warm = 8, timed = 4;
+        for (int round = 0; round < 2; ++round)
+            for (size_t c = 0; c < cand.size(); ++c) {
+                set_stream_lattices(s, cand[c][0], cand[c][1]);
+                for (int i = 0; i < (round == 0 && c == 0 ? warm : 1); ++i)
+                    HIP_CHECK(launch_stream2d(s.a3_int[i & 1], s.n3_int, spl, false, stream_cfg, s.s_comp));
+                HIP_CHECK(hipEventRecord(e0, s.s_comp));
+                for (int i = 0; i < timed; ++i)
+                    HIP_CHECK(launch_stream2d(s.a3_int[i & 1], s.n3_int, spl, false, stream_cfg, s.s_comp));
+                HIP_CHECK(hipEventRecord(e1, s.s_comp));
+                HIP_CHECK(hipEventSynchronize(e1));
+                float ms = 0.f;
+                HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+                best[c] = std::min(best[c], ms / timed);
+            }
+        HIP_CHECK(hipEventDestroy(e0));
+        HIP_CHECK(hipEventDestroy(e1));
+        size_t keep = 0;
+        for (size_t c = 1; c < cand.size(); ++c)
+            if (best[c] < best[keep]) keep = c;
+        probe_ms.assign(best.begin(), best.end());
+        probe_kept = (int)keep;
+        if (getenv("LBM_PLACEMENT_LOG")) {
+            fprintf(stderr, "lbm placement probe (%dx%d): ms per launch", s.w, s.h);
+            for (float v : best) fprintf(stderr, " %.4f", v);
+            fprintf(stderr, "; kept pair %d\n", probe_kept);
+        }
+        for (size_t c = 0; c < cand.size(); ++c)
+            if (c != keep)
+                for (float *p : cand[c]) HIP_CHECK(hipFree(p));
+        set_stream_lattices(s, cand[keep][0], cand[keep][1]);
+        for (float *p : cand[keep]) HIP_CHECK(hipMemset(p, 0, sizeof(float) * n));
+        build_args(s);
     }
 
     // `st` waits for the last exchange: own ghosts unpacked, and (LOCAL)
