@@ -1313,7 +1313,7 @@ struct lbm_handle {
     // sub-domain at one of two speed levels (about 7 % apart) set by the
     // physical pages under its lattices, fixed for the engine's life.  A single
     // sub-domain of at least 2^25 cells allocates LBM_PLACEMENT_TRIES (5; at most
-    // 48 GB of them) lattice pairs, all held at once, times the interior launch on each
+    // 96 GB of them) lattice pairs, all held at once, times the interior launch on each
     // (non-reducing form: av_local and the reduction control block are not
     // touched; constant populations; two interleaved rounds after a clock
     // warm-up, minimum per pair), keeps the fastest pair and frees the others.  The kept
