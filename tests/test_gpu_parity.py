@@ -686,3 +686,24 @@ def test_lattice_placement_knobs_bitwise(gpu_lib, env, monkeypatch):
         assert used == "stream"
         assert np.array_equal(cells, ref), kw
         np.testing.assert_allclose(av, ref_av, rtol=5e-5)
+
+
+def test_placement_probe_same_lattice(gpu_lib, monkeypatch):
+    """The placement probe (8192x4096 = 2^25 cells, the
+    smallest sub-domain it runs on) leaves the engine as if it had not run:
+    lattice and av_vels bitwise equal with and without it, 11 steps (two
+    5-step launches and a one-step remainder)."""
+    p = lio.Params(8192, 4096, 0, 11, 0.1, 0.005, 1.7)
+    obst = np.zeros((p.ny, p.nx), np.uint8)
+    obst[0, :] = obst[-1, :] = 1
+    obst[p.ny // 4: p.ny // 2, p.nx // 3] = 1
+    cells0 = lio.init_cells(p)
+    out = []
+    for tries in ("1", "3"):
+        monkeypatch.setenv("LBM_PLACEMENT_TRIES", tries)
+        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 11, devices=[0], kernel=gpu_lib.KERNEL_STREAM)
+        assert used == "stream"
+        out.append((cells, av))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.isfinite(out[1][1]).all()
