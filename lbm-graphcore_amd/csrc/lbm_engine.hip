@@ -1312,7 +1312,8 @@ struct lbm_handle {
     // Placement probe.  The stream kernel runs a large
     // sub-domain at one of two speed levels (about 7 % apart) set by the
     // physical pages under its lattices, fixed for the engine's life.  A single
-    // sub-domain of at least 2^25 cells allocates LBM_PLACEMENT_TRIES (5; at most
+    // sub-domain per process (one domain, or one RCCL rank's block: the probe
+    // launches touch only its own lattices and send buffers) of at least 2^25 cells allocates LBM_PLACEMENT_TRIES (5; at most
     // 96 GB of them) lattice pairs, all held at once, times the interior launch on each
     // (non-reducing form: av_local and the reduction control block are not
     // touched; constant populations; two interleaved rounds after a clock
@@ -1323,7 +1324,7 @@ struct lbm_handle {
         const size_t pair_bytes = 2 * sizeof(float) * (size_t)s.lattice_floats;
         const int cap = (int)std::max<size_t>(1, (48ull << 30) / pair_bytes);  // at most 48 GB of candidates
         const int tries = std::min({std::max(env_int("LBM_PLACEMENT_TRIES", 5), 1), 8, cap});
-        if (tries <= 1 || !use_stream || stream_v != 3 || subs.size() != 1 || multi() || s.f_joint ||
+        if (tries <= 1 || !use_stream || stream_v != 3 || subs.size() != 1 || s.f_joint ||
             (long long)s.w * s.h < (1LL << 25) || s.n3_int <= 0)
             return;
         const size_t n = (size_t)s.lattice_floats;

@@ -688,11 +688,13 @@ def test_lattice_placement_knobs_bitwise(gpu_lib, env, monkeypatch):
         np.testing.assert_allclose(av, ref_av, rtol=5e-5)
 
 
-def test_placement_probe_same_lattice(gpu_lib, monkeypatch):
+@pytest.mark.parametrize("transport", ["local", "rccl"])
+def test_placement_probe_same_lattice(gpu_lib, transport, monkeypatch):
     """The placement probe (8192x4096 = 2^25 cells, the
     smallest sub-domain it runs on) leaves the engine as if it had not run:
     lattice and av_vels bitwise equal with and without it, 11 steps (two
-    5-step launches and a one-step remainder)."""
+    5-step launches and a one-step remainder); also as a one-rank RCCL block
+    whose periodic wraps go through self send/recv."""
     p = lio.Params(8192, 4096, 0, 11, 0.1, 0.005, 1.7)
     obst = np.zeros((p.ny, p.nx), np.uint8)
     obst[0, :] = obst[-1, :] = 1
@@ -701,7 +703,11 @@ def test_placement_probe_same_lattice(gpu_lib, monkeypatch):
     out = []
     for tries in ("1", "3"):
         monkeypatch.setenv("LBM_PLACEMENT_TRIES", tries)
-        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 11, devices=[0], kernel=gpu_lib.KERNEL_STREAM)
+        kw = dict(devices=[0], kernel=gpu_lib.KERNEL_STREAM)
+        if transport == "rccl":
+            kw.update(transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1, unique_id=gpu_lib.rccl_unique_id(),
+                      flags=gpu_lib.FLAG_FORCE_EXCHANGE)
+        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 11, **kw)
         assert used == "stream"
         out.append((cells, av))
     assert np.array_equal(out[0][0], out[1][0])
