@@ -12,6 +12,7 @@ from lbm_amd import native  # noqa: E402
 from oracle import oracle  # noqa: E402  (checker only)
 import test_d3q19 as T  # noqa: E402
 
+# ENVS[4] named the contiguous-allocation knob of an intermediate build (removed; now a no-op)
 ENVS = [{}, {"LBM3D_KSPAD": "320"}, {"LBM3D_KSPAD": "64"}, {"LBM_LATTICE_PAD": "4096"},
         {"LBM_LATTICE_CONTIG": "1", "LBM3D_KSPAD": "64"}]
 seq = sys.argv[1] if len(sys.argv) > 1 else "full"
