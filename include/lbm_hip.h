@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LBM_ABI_VERSION 3
+#define LBM_ABI_VERSION 4
 
 enum {
     LBM_OK = 0,
@@ -115,6 +115,17 @@ typedef struct lbm_config {
 #define LBM_FLAG_FORCE_EXCHANGE 1
 /* One time step per launch (no fused two-step kernel). */
 #define LBM_FLAG_ONE_STEP 2
+/* fp32 tolerance mode of the STREAM kernel (north_star: "within a stated fp32
+ * tolerance"): one reciprocal of the density per cell
+ * (v_rcp_f32 + one Newton step) shared by u_x and u_y instead of two
+ * correctly rounded divisions, the constant divisions by 9 and 36 folded into
+ * multiplications, and FMA contraction.  Still IEEE fp32 arithmetic, but no
+ * longer bitwise equal to LastChance.cpp:226-262: after 100 steps at 8192^2
+ * every population stays within 2e-6 relative of the oracle, and check.py
+ * passes on all four reference grids (tests/test_gpu_tolerance.py).  Other
+ * kernels (remainder one-step launches, RESIDENT, STEP2) stay bitwise.
+ * lbm_numerics() reports which mode a handle runs. */
+#define LBM_FLAG_TOLERANCE 4
 
 typedef struct lbm_handle lbm_handle;
 
@@ -230,6 +241,25 @@ int lbm_local_rects(lbm_handle *h, lbm_rect *rects, int32_t max_rects, int32_t *
  * the first run). */
 int32_t lbm_kernel_in_use(lbm_handle *h);
 int32_t lbm_steps_per_launch(lbm_handle *h);
+
+/* Launches of the last lbm_run / lbm_run_steps: fused (steps_per_launch
+ * steps each; RESIDENT: the one persistent launch) and one-step (the
+ * remainder of a step count that is not a multiple, or every step in
+ * one-step modes).  Lets a test prove which kernel advanced the lattice. */
+int lbm_run_stats(lbm_handle *h, int32_t *fused_launches, int32_t *one_step_launches);
+
+/* Placement probe of lbm_create: the candidate lattice pair kept
+ * (-1: no probe ran), how many pairs were timed, and (up to max_ms of) their
+ * ms per launch. */
+int lbm_placement_probe(lbm_handle *h, int32_t *kept, int32_t *tried, float *ms_per_launch, int32_t max_ms);
+
+/* 0: every kernel of the handle is bitwise equal to the CPU oracle; 1: the
+ * fused launches run the LBM_FLAG_TOLERANCE collision. */
+int32_t lbm_numerics(lbm_handle *h);
+
+/* Hash of the library's sources (csrc/, include/) at build time; the Python
+ * binding refuses a library whose hash differs from the sources beside it. */
+const char *lbm_source_hash(void);
 
 const char *lbm_last_error(lbm_handle *h);
 

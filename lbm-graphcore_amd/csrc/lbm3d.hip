@@ -618,6 +618,8 @@ struct lbm3d_handle {
     bool skip = false; // LBM3D_SKIP: waves skip the collisions of rows no later level reads (not faster)
     int pd = 1;        // LBM3D_PD: input planes in flight in the two-step kernel (1, 2)
     long long kspad = 0;  // LBM3D_KSPAD: floats appended to each speed plane (multiple of 64)
+    const char *lattice_pad = nullptr;  // LBM_LATTICE_PAD (debug knob)
+    bool poison = false;  // LBM_POISON=1: fresh allocations filled with NaN bytes
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
     ncclComm_t comm = nullptr;
@@ -649,16 +651,32 @@ struct lbm3d_handle {
         free_cells = 0;
         for (long long i = 0; i < cells; ++i) free_cells += obstacles[i] ? 0 : 1;
         px = (p.nx + 15) / 16 * 16;  // 64-byte rows
-        const char *pe = getenv("LBM3D_PAIR");
-        pair = p.nx % 2 == 0 && !(pe && *pe && atoi(pe) == 0);
-        if (const char *z = getenv("LBM3D_ZB")) zb = (atoi(z) == 1 || atoi(z) == 4 || atoi(z) == 8) ? atoi(z) : 2;
-        if (const char *n = getenv("LBM3D_NT")) nt = atoi(n) != 0;
-        if (const char *t = getenv("LBM3D_TWO")) two = atoi(t) != 0;
-        if (const char *g = getenv("LBM3D_SEG")) seg = std::max(1, atoi(g));
-        if (const char *h = getenv("LBM3D_TH")) th = (atoi(h) == 14 || atoi(h) == 15) ? atoi(h) : 12;
-        if (const char *k = getenv("LBM3D_SKIP")) skip = atoi(k) != 0;
-        if (const char *d = getenv("LBM3D_PD")) pd = atoi(d) == 2 ? 2 : 1;
-        if (const char *k = getenv("LBM3D_KSPAD")) kspad = (std::max(0LL, atoll(k)) + 63) / 64 * 64;
+        // tuning knobs only with LBM_DEBUG_KNOBS=1 (as the 2-D engine); LBM_POISON always
+        const char *dk = getenv("LBM_DEBUG_KNOBS");
+        const bool knobs = dk && *dk && atoi(dk) != 0;
+        const char *po = getenv("LBM_POISON");
+        poison = po && *po && atoi(po) != 0;
+        auto knob = [&](const char *name) -> const char * {
+            const char *v = knobs ? getenv(name) : nullptr;
+            return (v && *v) ? v : nullptr;
+        };
+        const char *pe = knob("LBM3D_PAIR");
+        pair = p.nx % 2 == 0 && !(pe && atoi(pe) == 0);
+        if (const char *z = knob("LBM3D_ZB")) zb = (atoi(z) == 1 || atoi(z) == 4 || atoi(z) == 8) ? atoi(z) : 2;
+        if (const char *n = knob("LBM3D_NT")) nt = atoi(n) != 0;
+        if (const char *t = knob("LBM3D_TWO")) two = atoi(t) != 0;
+        if (const char *g = knob("LBM3D_SEG")) seg = std::max(1, atoi(g));
+        if (const char *h = knob("LBM3D_TH")) th = atoi(h);
+        if (const char *k = knob("LBM3D_SKIP")) skip = atoi(k) != 0;
+        if (const char *d = knob("LBM3D_PD")) pd = atoi(d);
+        if (const char *k = knob("LBM3D_KSPAD")) kspad = (std::max(0LL, atoll(k)) + 63) / 64 * 64;
+        lattice_pad = knob("LBM_LATTICE_PAD");
+        // the two-step kernel is instantiated for these (rows, skip, prefetch)
+        // combinations only; anything else is rejected here, never launched as
+        // a different template (blocks of 64 x th threads, at most 960)
+        if (two_variant(th, skip, pd) < 0)
+            throw fail3(LBM_E_INVALID, "unsupported two-step block: LBM3D_TH " + std::to_string(th) + ", SKIP " +
+                                           std::to_string(skip ? 1 : 0) + ", PD " + std::to_string(pd));
         KS = (long long)p.ny * px + kspad;
         PL = (long long)Q3 * KS;
         // round-robin z extents (StructuredGridUtils.hpp:161-165 rule, in z)
@@ -725,22 +743,30 @@ struct lbm3d_handle {
 
     void alloc(Slab &s, const uint8_t *obstacles) {
         H3(hipSetDevice(s.dev));
+        // streams first: every initial fill below is ordered on s_comp (a
+        // null-stream hipMemset is not ordered with these non-blocking streams)
+        H3(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
+        H3(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
+        int lo = 0, hi = 0;
+        H3(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        H3(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, hi));
+        for (hipEvent_t *e : {&s.ev_b, &s.ev_i, &s.ev_x, &s.ev_end}) H3(hipEventCreateWithFlags(e, hipEventDisableTiming));
         // two ghost planes below and above (the two-step kernel reads both)
         const size_t floats = (size_t)(s.nzs + 4) * PL;
-        const char *lp = getenv("LBM_LATTICE_PAD");
+        const char *lp = lattice_pad;
         if (lp && *lp) {
             // both lattices in one allocation, the second pad bytes (rounded to
             // 256 B) after the end of the first (see lbm_engine.hip alloc_sub)
             const size_t second = floats + (size_t)(std::max(0LL, atoll(lp)) + 255) / 256 * 64;
             const size_t n = (second + floats) * sizeof(float);
             H3(hipMalloc(&s.f[0], n));
-            H3(hipMemset(s.f[0], 0, n));
+            fill_fresh(s.f[0], n, s.s_comp);
             s.f[1] = s.f[0] + second;
             s.f_joint = true;
         } else {
             for (int k = 0; k < 2; ++k) {
                 H3(hipMalloc(&s.f[k], floats * sizeof(float)));
-                H3(hipMemset(s.f[k], 0, floats * sizeof(float)));
+                fill_fresh(s.f[k], floats * sizeof(float), s.s_comp);
             }
         }
         for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + 2 * PL;
@@ -758,15 +784,19 @@ struct lbm3d_handle {
         s.nblk_int = multi() ? blocks_for(s.nzs - 2) : 0;
         s.nblk_all = multi() ? s.nblk_bnd + s.nblk_int : blocks_for(s.nzs);
         H3(hipMalloc(&s.partials, sizeof(float) * (size_t)(s.nblk_all + 64)));
+        fill_fresh(s.partials, sizeof(float) * (size_t)(s.nblk_all + 64), s.s_comp);
         s.nblk_two = 0;
         for (const auto &r : two_ranges(s)) s.nblk_two += two_blocks(r.first, r.second);
         H3(hipMalloc(&s.partials2, sizeof(float) * (2 * (size_t)std::max(s.nblk_two, 1) + 64)));
-        H3(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
-        H3(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
-        int lo = 0, hi = 0;
-        H3(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        H3(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, hi));
-        for (hipEvent_t *e : {&s.ev_b, &s.ev_i, &s.ev_x, &s.ev_end}) H3(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        fill_fresh(s.partials2, sizeof(float) * (2 * (size_t)std::max(s.nblk_two, 1) + 64), s.s_comp);
+    }
+
+    // Initial fill of a fresh allocation on `st`, waited for: zero, or with
+    // LBM_POISON=1 all-ones bytes (NaN floats) -- a read of anything the
+    // engine did not write then shows up as NaN (tests/test_poison.py).
+    void fill_fresh(void *ptr, size_t bytes, hipStream_t st) const {
+        H3(hipMemsetAsync(ptr, poison ? 0xFF : 0, bytes, st));
+        H3(hipStreamSynchronize(st));
     }
 
     // Output plane ranges of one two-step pass of slab s, in launch order.
@@ -779,6 +809,15 @@ struct lbm3d_handle {
         std::vector<std::pair<int, int>> r = {{0, 2}, {s.nzs - 2, s.nzs}};
         if (s.nzs > 4) r.push_back({2, s.nzs - 2});
         return r;
+    }
+    // switch key of the instantiated step3d_two<TH, SKIP, PD> variants, -1 if none
+    static int two_variant(int th, bool skip, int pd) {
+        if ((th != 12 && th != 14 && th != 15) || (pd != 1 && pd != 2)) return -1;
+        const int key = (th * 2 + (skip ? 1 : 0)) * 2 + (pd - 1);
+        switch (key) {
+            case 48: case 49: case 50: case 51: case 56: case 58: case 59: case 60: case 62: case 63: return key;
+            default: return -1;
+        }
     }
     int two_blocks(int z0, int zn) const {
         return ((p.nx + T3OX - 1) / T3OX) * ((p.ny + th - 5) / (th - 4)) * ((zn - z0 + seg - 1) / seg);
@@ -816,7 +855,7 @@ struct lbm3d_handle {
         a.blk0 = blk0;
         const dim3 g((p.nx + T3OX - 1) / T3OX, (p.ny + th - 5) / (th - 4), (zn - z0 + seg - 1) / seg);
         const dim3 b(T3W, th);
-        switch ((th * 2 + (skip ? 1 : 0)) * 2 + (pd - 1)) {
+        switch (two_variant(th, skip, pd)) {
             case 48: hipLaunchKernelGGL((step3d_two<12, false, 1>), g, b, 0, st, a); break;
             case 49: hipLaunchKernelGGL((step3d_two<12, false, 2>), g, b, 0, st, a); break;
             case 50: hipLaunchKernelGGL((step3d_two<12, true, 1>), g, b, 0, st, a); break;
@@ -827,7 +866,7 @@ struct lbm3d_handle {
             case 60: hipLaunchKernelGGL((step3d_two<15, false, 1>), g, b, 0, st, a); break;
             case 62: hipLaunchKernelGGL((step3d_two<15, true, 1>), g, b, 0, st, a); break;
             case 63: hipLaunchKernelGGL((step3d_two<15, true, 2>), g, b, 0, st, a); break;
-            default: hipLaunchKernelGGL((step3d_two<12, true, 1>), g, b, 0, st, a); break;
+            default: throw fail3(LBM_E_INTERNAL, "unvalidated two-step variant");
         }
         H3(hipGetLastError());
     }
@@ -941,7 +980,7 @@ struct lbm3d_handle {
             if (s.av_local) H3(hipFree(s.av_local));
             s.av_cap = std::max(n, 1);
             H3(hipMalloc(&s.av_local, sizeof(float) * (size_t)s.av_cap));
-            H3(hipMemset(s.av_local, 0, sizeof(float) * (size_t)s.av_cap));
+            fill_fresh(s.av_local, sizeof(float) * (size_t)s.av_cap, s.s_comp);
         }
     }
 

@@ -47,8 +47,8 @@ hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t
 hipError_t launch_stream(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
 hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s);
 hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n);
-hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, hipStream_t s);
-hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n);
+hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s);
+hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n);
 hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, hipStream_t s);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
@@ -227,6 +227,10 @@ struct lbm_handle {
     hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
     std::vector<float> probe_ms;  // placement probe: ms per launch of each lattice pair tried
     int probe_kept = -1;          // the pair kept (-1: no probe)
+    bool debug_knobs = false;     // LBM_DEBUG_KNOBS=1: the tuning knobs below are read from the environment
+    bool poison = false;          // LBM_POISON=1: fresh allocations filled with NaN bytes (read-before-write check)
+    bool tolerance = false;       // LBM_FLAG_TOLERANCE: stream kernel with the reciprocal collision (not bitwise)
+    int run_fused = 0, run_single = 0;  // launches of the last run: fused (spl steps) / one-step
     // Tuning knobs (environment, read at create): LBM_TWO_STEP, LBM_MAX_BLOCKS,
     // LBM_LAYOUT (rows|planar), LBM_GRAPH_STEPS, LBM_FORCE_EXCHANGE.  Defaults
     // chosen with tools/ab_bench.py on MI355X (profiles/r01/ab_*.log).
@@ -251,25 +255,49 @@ struct lbm_handle {
     // ------------------------------------------------------------------
     void set_device(const Sub &s) const { HIP_CHECK(hipSetDevice(s.dev)); }
 
+    // Initial fill of a fresh device allocation, ordered on `st` and waited
+    // for (the engine's streams are non-blocking: a null-stream hipMemset is
+    // not ordered with them).  Zero, or with LBM_POISON=1 all-ones bytes (a
+    // NaN in every float), so that a value the engine reads without having
+    // written it shows up as NaN in the lattice or in av_vels (SURVEY §5
+    // sanitizer row; tests/test_poison.py).
+    void fill_fresh(void *ptr, size_t bytes, hipStream_t st) const {
+        HIP_CHECK(hipMemsetAsync(ptr, poison ? 0xFF : 0, bytes, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
+    // Protocol words whose zero IS their initialisation (control block, status)
+    static void fill_zero(void *ptr, size_t bytes, hipStream_t st) {
+        HIP_CHECK(hipMemsetAsync(ptr, 0, bytes, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
+
     static int env_int(const char *name, int dflt) {
         const char *v = getenv(name);
         return (v && *v) ? atoi(v) : dflt;
     }
+    // Tuning / A-B knobs are read only with LBM_DEBUG_KNOBS=1:
+    // without it the library ignores the environment and runs its defaults
+    // (LBM_POISON, a read-before-write check that changes no result of a
+    // correct engine, is the one exception).
+    int knob(const char *name, int dflt) const { return debug_knobs ? env_int(name, dflt) : dflt; }
+    const char *knob_str(const char *name) const { return debug_knobs ? getenv(name) : nullptr; }
 
     void read_tuning() {
-        max_blocks_cfg = std::max(1, env_int("LBM_MAX_BLOCKS", max_blocks_cfg));
-        graph_steps = std::max(0, env_int("LBM_GRAPH_STEPS", graph_steps));
-        fused = env_int("LBM_TWO_STEP", fused ? 1 : 0) != 0;
-        tile2 = std::min(std::max(env_int("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
-        xoff = std::max(MAX_GR, (env_int("LBM_XOFF", xoff) + 3) / 4 * 4);
-        stream_s = std::min(std::max(env_int("LBM_STREAM_S", stream_s), 2), 6);
-        stream_hs = std::max(0, env_int("LBM_STREAM_HS", stream_hs));
-        stream_v = std::min(std::max(env_int("LBM_STREAM_V", stream_v), 1), 3);
-        stream_waves = env_int("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
-        stream_cfg = std::min(std::max(env_int("LBM_STREAM_CFG", stream_cfg), 0), 3);
-        stream_min_cells = std::max(0, env_int("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
+        debug_knobs = env_int("LBM_DEBUG_KNOBS", 0) != 0;
+        poison = env_int("LBM_POISON", 0) != 0;
+        max_blocks_cfg = std::max(1, knob("LBM_MAX_BLOCKS", max_blocks_cfg));
+        graph_steps = std::max(0, knob("LBM_GRAPH_STEPS", graph_steps));
+        fused = knob("LBM_TWO_STEP", fused ? 1 : 0) != 0;
+        tile2 = std::min(std::max(knob("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
+        xoff = std::max(MAX_GR, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
+        stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 6);
+        stream_hs = std::max(0, knob("LBM_STREAM_HS", stream_hs));
+        stream_v = std::min(std::max(knob("LBM_STREAM_V", stream_v), 1), 3);
+        stream_waves = knob("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
+        stream_cfg = std::min(std::max(knob("LBM_STREAM_CFG", stream_cfg), 0), 3);
+        stream_min_cells = std::max(0, knob("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
-            const char *g = getenv("LBM_STREAM_GUIDE");
+            const char *g = knob_str("LBM_STREAM_GUIDE");
             std::string spec = g ? std::string(g) : std::string("96:0.85,32:0.1,10");
             guide.clear();
             if (spec != "0") {
@@ -286,19 +314,19 @@ struct lbm_handle {
                 }
             }
         }
-        res_th_env = std::max(0, env_int("LBM_RES_TH", 0));
-        res_version = env_int("LBM_RES_V", 0);
-        res_per_cu = std::min(std::max(env_int("LBM_RES_PER_CU", res_per_cu), 1), 2);
-        res_early_poll = env_int("LBM_RES_EARLY", res_early_poll) != 0 ? 1 : 0;
-        resident_max_cells = std::max(0, env_int("LBM_RES_MAX_CELLS", (int)resident_max_cells));
-        if (const char *k = getenv("LBM_KERNEL")) {
+        res_th_env = std::max(0, knob("LBM_RES_TH", 0));
+        res_version = knob("LBM_RES_V", 0);
+        res_per_cu = std::min(std::max(knob("LBM_RES_PER_CU", res_per_cu), 1), 2);
+        res_early_poll = knob("LBM_RES_EARLY", res_early_poll) != 0 ? 1 : 0;
+        resident_max_cells = std::max(0, knob("LBM_RES_MAX_CELLS", (int)resident_max_cells));
+        if (const char *k = knob_str("LBM_KERNEL")) {
             const std::string v(k);
             env_kernel = v == "pipeline" ? LBM_KERNEL_PIPELINE
                        : v == "resident" ? LBM_KERNEL_RESIDENT
                        : v == "stream" ? LBM_KERNEL_STREAM : v == "step2" ? LBM_KERNEL_STEP2
                        : v == "vec4" ? LBM_KERNEL_VEC4 : v == "scalar" ? LBM_KERNEL_SCALAR : -1;
         }
-        const char *l = getenv("LBM_LAYOUT");
+        const char *l = knob_str("LBM_LAYOUT");
         if (l && *l) row_interleaved = std::string(l) != "planar";
     }
 
@@ -516,6 +544,9 @@ struct lbm_handle {
         b3.accel_g = p.ny >= 2 ? p.ny - 2 : -1;
         b3.omega = p.omega;
         b3.omo = 1 - p.omega;
+        b3.tc0 = p.omega * (4.f / 9.f);
+        b3.tc1 = p.omega * (1.f / 9.f);
+        b3.tc2 = p.omega * (1.f / 36.f);
         b3.w1 = w1;
         b3.w2 = w2;
         b3.ctl = s.ctl;
@@ -536,7 +567,7 @@ struct lbm_handle {
         for (int k = 0; k < 2; ++k) {
             if (s.partials[k]) HIP_CHECK(hipFree(s.partials[k]));
             HIP_CHECK(hipMalloc(&s.partials[k], sizeof(float) * (size_t)cap));
-            HIP_CHECK(hipMemset(s.partials[k], 0, sizeof(float) * (size_t)cap));
+            fill_fresh(s.partials[k], sizeof(float) * (size_t)cap, s.s_comp);
         }
         for (int par = 0; par < 2; ++par) {
             const float *fin = s.o[par];
@@ -579,7 +610,7 @@ struct lbm_handle {
             if (!s.dst2_dev) HIP_CHECK(hipMalloc(&s.dst2_dev, sizeof(Dst2) * 16));
             HIP_CHECK(hipMemcpy(s.dst2_dev + 8 * par, si.dst, sizeof(Dst2) * 8, hipMemcpyHostToDevice));
             si.dstg = sb.dstg = s.dst2_dev + 8 * par;
-            if (getenv("LBM_STREAM_TRACE") && use_stream && s.n3_int > 0) {
+            if (knob_str("LBM_STREAM_TRACE") && use_stream && s.n3_int > 0) {
                 if (!s.trace) HIP_CHECK(hipMalloc(&s.trace, sizeof(unsigned long long) * 2 * (size_t)s.n3_int));
                 si.trace = s.trace;
             }
@@ -590,7 +621,7 @@ struct lbm_handle {
         }
         // v3: which work units read an obstacle cell (the rest run without
         // rebound selects); obstacles and the work split are fixed from here on
-        const char *uo = getenv("LBM_STREAM_UOBST");
+        const char *uo = knob_str("LBM_STREAM_UOBST");
         if (use_stream && stream_v == 3 && !(uo && atoi(uo) == 0)) {
             if (s.uobst) HIP_CHECK(hipFree(s.uobst));
             const int ni = std::max(0, s.a3_int[0].total), nb = std::max(0, s.a3_bnd[0].total);
@@ -605,7 +636,7 @@ struct lbm_handle {
             // dispatch order: within each XCD's range of slots (xcd_remap),
             // the units that read obstacle cells (slower: rebound selects)
             // first, the rest after, each group in its original order
-            const char *so = getenv("LBM_STREAM_ORDER");
+            const char *so = knob_str("LBM_STREAM_ORDER");
             if (!(so && atoi(so) == 0)) {
                 std::vector<uint8_t> fl((size_t)ni + nb);
                 HIP_CHECK(hipMemcpy(fl.data(), s.uobst, fl.size(), hipMemcpyDeviceToHost));
@@ -667,7 +698,7 @@ struct lbm_handle {
             // (profiles/r01/stream/ab_hs_rounds.log).  Eight rounds where the
             // segments stay at least 4S rows high, fewer otherwise.
             int per_cu = 0, cus = 0;
-            const hipError_t occ = stream_v == 3 ? stream2d_blocks_per_cu(S, stream_cfg, per_cu)
+            const hipError_t occ = stream_v == 3 ? stream2d_blocks_per_cu(S, stream_cfg, tolerance, per_cu)
                                                  : stream2c_blocks_per_cu(S, stream_waves, per_cu);
             if (stream_v >= 2 && occ == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev) == hipSuccess &&
@@ -679,7 +710,7 @@ struct lbm_handle {
                 const long long nseg = std::min(nseg_max, std::max<long long>(1, k * cap / strips));
                 hs = (int)((rows + nseg - 1) / nseg);
             }
-            if (getenv("LBM_STREAM_DEBUG"))
+            if (knob_str("LBM_STREAM_DEBUG"))
                 fprintf(stderr, "[stream split] %dx%d: strips %lld rows %lld waves/CU %d CUs %d -> hs %d\n", s.w, s.h,
                         strips, rows, per_cu, cus, hs);
         }
@@ -719,6 +750,10 @@ struct lbm_handle {
         const int hb = h / NB;
         if (hb < 2 * guide[0].first) return false;
         const auto rows = round_robin(h, NB);
+        // built apart and appended only when every tier rect fits, so a guide
+        // with too many tiers leaves `out` untouched and the caller falls back
+        // to uniform heights
+        std::vector<SRect> tiers;
         int y = y0;
         for (int band = 0; band < NB; ++band) {
             int rest = rows[band];
@@ -726,12 +761,14 @@ struct lbm_handle {
                 const int ht = std::max(1, guide[k].first);
                 int r = rest;
                 if (k + 1 < guide.size()) r = std::min(rest, std::max(ht, (int)(rows[band] * guide[k].second) / ht * ht));
-                out.push_back(mk(x0, y, w, r, ht));
+                tiers.push_back(mk(x0, y, w, r, ht));
                 y += r;
                 rest -= r;
             }
         }
-        return (int)out.size() <= MAX_SRECTS;
+        if ((int)(out.size() + tiers.size()) > MAX_SRECTS) return false;
+        out.insert(out.end(), tiers.begin(), tiers.end());
+        return true;
     }
 
     int fill_srects(StreamArgs &a, const std::vector<SRect> &rs) const {
@@ -759,7 +796,7 @@ struct lbm_handle {
             if (s.av_local) HIP_CHECK(hipFree(s.av_local));
             s.av_cap = std::max(n, 1);
             HIP_CHECK(hipMalloc(&s.av_local, sizeof(float) * (size_t)s.av_cap));
-            HIP_CHECK(hipMemset(s.av_local, 0, sizeof(float) * (size_t)s.av_cap));
+            fill_fresh(s.av_local, sizeof(float) * (size_t)s.av_cap, s.s_comp);
             for (int par = 0; par < 2; ++par) {
                 s.a1_int[par].av_local = s.av_local;
                 s.a1_bnd[par].av_local = s.av_local;
@@ -783,7 +820,8 @@ struct lbm_handle {
         if (cfg.graph_steps > 0) graph_steps = cfg.graph_steps;
         if (cfg.graph_steps < 0) graph_steps = 0;
         if (cfg.flags & LBM_FLAG_ONE_STEP) fused = false;
-        force_exchange = (cfg.flags & LBM_FLAG_FORCE_EXCHANGE) != 0 || env_int("LBM_FORCE_EXCHANGE", 0) != 0;
+        force_exchange = (cfg.flags & LBM_FLAG_FORCE_EXCHANGE) != 0 || knob("LBM_FORCE_EXCHANGE", 0) != 0;
+        tolerance = (cfg.flags & LBM_FLAG_TOLERANCE) != 0;
         if (partition(p.nx, p.ny, parts, cfg.grid_rows, cfg.grid_cols, R, C, all_rects) != LBM_OK)
             throw lbm_failure(LBM_E_INVALID, "cannot partition " + std::to_string(p.nx) + "x" + std::to_string(p.ny) +
                                                  " into " + std::to_string(parts) + " parts");
@@ -902,6 +940,7 @@ struct lbm_handle {
             for (auto &s : subs) {
                 set_device(s);
                 HIP_CHECK(hipMalloc(&s.pipe_partials, sizeof(float) * (size_t)round_up(pipe_blocks(s.w, s.h), 4)));
+                fill_fresh(s.pipe_partials, sizeof(float) * (size_t)round_up(pipe_blocks(s.w, s.h), 4), s.s_comp);
             }
         // lattice-resident kernel: one sub-domain whose 64-column tiles can all be co-resident
         const bool res_ok = parts == 1 && !force_exchange && subs.size() == 1 && !pipeline;
@@ -962,10 +1001,12 @@ struct lbm_handle {
         }
         if (res_variant < 0) return false;
         const size_t granules = 2ull * res_tx * res_ty * 8 * 3 * RES_GW;
+        // granules validate by their step tag (== the expected step, never 0 or
+        // all-ones in a run): the poison pattern reads as "not there yet"
         HIP_CHECK(hipMalloc(&res_halo, granules * sizeof(unsigned long long)));
-        HIP_CHECK(hipMemset(res_halo, 0, granules * sizeof(unsigned long long)));
+        fill_fresh(res_halo, granules * sizeof(unsigned long long), s.s_comp);
         HIP_CHECK(hipMalloc(&res_status, 64));
-        HIP_CHECK(hipMemset(res_status, 0, 64));
+        fill_zero(res_status, 64, s.s_comp);
         int khz = 0;
         HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.dev));
         res_timeout = (long long)std::max(khz, 1000) * 2000;  // 2 s of wall clock per poll phase
@@ -1018,7 +1059,7 @@ struct lbm_handle {
             long long *trace = nullptr;
             unsigned long long *htrace = nullptr;
             const int trace_steps = std::min(steps, 256);
-            const int trace_mode = env_int("LBM_RES_TRACE", 0);
+            const int trace_mode = knob("LBM_RES_TRACE", 0);
             if (trace_mode) {
                 HIP_CHECK(hipMalloc(&trace, sizeof(long long) * 5 * trace_steps));
                 HIP_CHECK(hipMemsetAsync(trace, 0, sizeof(long long) * 5 * trace_steps, s.s_comp));
@@ -1152,6 +1193,17 @@ struct lbm_handle {
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
         set_device(s);
+        // streams first: every initial fill below is ordered on s_comp
+        HIP_CHECK(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
+        int prio_lo = 0, prio_hi = 0;
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIP_CHECK(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, prio_hi));
+        HIP_CHECK(hipEventCreateWithFlags(&s.ev_b, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&s.ev_i, hipEventDisableTiming));
+        for (auto &e : s.ev_bp) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&s.ev_u, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&s.ev_end, hipEventDisableTiming));
         // two spare columns past the ring: a two-column stream lane reads its
         // pair unclamped up to column w + gr
         s.rf = (int)round_up(s.w + xoff + gr + 2, 64);
@@ -1169,20 +1221,20 @@ struct lbm_handle {
             s.lattice_floats = Q * s.plane;
         }
         s.origin_off = (long long)gr * s.pitch + xoff;
-        const char *lp = getenv("LBM_LATTICE_PAD");
+        const char *lp = knob_str("LBM_LATTICE_PAD");
         if (lp && *lp) {
             // both lattices in one allocation, the second pad bytes (rounded to
             // 256 B) after the end of the first
             const long long second = s.lattice_floats + (std::max(0LL, atoll(lp)) + 255) / 256 * 64;
             const size_t n = sizeof(float) * (size_t)(second + s.lattice_floats);
             HIP_CHECK(hipMalloc(&s.f[0], n));
-            HIP_CHECK(hipMemset(s.f[0], 0, n));
+            fill_fresh(s.f[0], n, s.s_comp);
             s.f[1] = s.f[0] + second;
             s.f_joint = true;
         } else {
             for (int k = 0; k < 2; ++k) {
                 HIP_CHECK(hipMalloc(&s.f[k], sizeof(float) * (size_t)s.lattice_floats));
-                HIP_CHECK(hipMemset(s.f[k], 0, sizeof(float) * (size_t)s.lattice_floats));
+                fill_fresh(s.f[k], sizeof(float) * (size_t)s.lattice_floats, s.s_comp);
             }
         }
         for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + s.origin_off;
@@ -1218,24 +1270,14 @@ struct lbm_handle {
         }
         if (total > 0) {
             HIP_CHECK(hipMalloc(&s.halo_mem, sizeof(float) * (size_t)total));
-            HIP_CHECK(hipMemset(s.halo_mem, 0, sizeof(float) * (size_t)total));
+            fill_fresh(s.halo_mem, sizeof(float) * (size_t)total, s.s_comp);
             for (int d = 0; d < 8; ++d) {
                 s.send[d] = s.remote[d] ? s.halo_mem + off_send[d] : nullptr;
                 s.recv[d] = s.remote[d] ? s.halo_mem + off_recv[d] : nullptr;
             }
         }
         HIP_CHECK(hipMalloc(&s.ctl, 64));
-        HIP_CHECK(hipMemset(s.ctl, 0, 64));
-        HIP_CHECK(hipStreamCreateWithFlags(&s.s_comp, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&s.s_comm, hipStreamNonBlocking));
-        int prio_lo = 0, prio_hi = 0;
-        HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-        HIP_CHECK(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, prio_hi));
-        HIP_CHECK(hipEventCreateWithFlags(&s.ev_b, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&s.ev_i, hipEventDisableTiming));
-        for (auto &e : s.ev_bp) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&s.ev_u, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&s.ev_end, hipEventDisableTiming));
+        fill_zero(s.ctl, 64, s.s_comp);
     }
 
     Sub *local_sub(int id) {
@@ -1320,65 +1362,110 @@ struct lbm_handle {
     // warm-up, minimum per pair), keeps the fastest pair and frees the others.  The kept
     // pair is zeroed and the launch arguments are rebuilt, so the engine state
     // is as if the probe had not run.  LBM_PLACEMENT_TRIES=1 turns it off.
+    // Scope: the single-sub-domain 2-D stream engine only.  LOCAL multi-sub
+    // engines are the one-GPU loop-back test mode (their sub-domains share one
+    // device and a probe would time them against each other), the D3Q19 engine
+    // showed no two-level spread worth a probe (38.9-42.0 GLUPS over seven
+    // placements at 512^3, profiles/r02/placement/d3.log, inside its +-10 %
+    // build-to-build noise).
     void placement_probe(Sub &s) {
         const size_t pair_bytes = 2 * sizeof(float) * (size_t)s.lattice_floats;
-        const int cap = (int)std::max<size_t>(1, (48ull << 30) / pair_bytes);  // at most 48 GB of candidates
-        const int tries = std::min({std::max(env_int("LBM_PLACEMENT_TRIES", 5), 1), 8, cap});
+        // at most 96 GB of candidate pairs held at once (a third of HBM):
+        // five at 8192^2 (4.9 GB per pair), four at 16384^2 (19.5 GB)
+        const int cap = (int)std::max<size_t>(1, (96ull << 30) / pair_bytes);
+        const int tries = std::min({std::max(knob("LBM_PLACEMENT_TRIES", 5), 1), 8, cap});
         if (tries <= 1 || !use_stream || stream_v != 3 || subs.size() != 1 || s.f_joint ||
             (long long)s.w * s.h < (1LL << 25) || s.n3_int <= 0)
             return;
         const size_t n = (size_t)s.lattice_floats;
         std::vector<std::array<float *, 2>> cand{{s.f[0], s.f[1]}};
-        for (int c = 1; c < tries; ++c) {
-            std::array<float *, 2> f{nullptr, nullptr};
-            if (hipMalloc(&f[0], sizeof(float) * n) != hipSuccess) { (void)hipGetLastError(); break; }
-            if (hipMalloc(&f[1], sizeof(float) * n) != hipSuccess) {
-                (void)hipGetLastError();
-                (void)hipFree(f[0]);
-                break;
-            }
-            cand.push_back(f);
-        }
-        const unsigned fill = 0x3dcccccdu;  // 0.1f: rho = 0.9 everywhere, no tiny-density path
-        for (auto &f : cand)
-            for (float *p : f) HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), (int)fill, n, s.s_comp));
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        HIP_CHECK(hipEventCreate(&e0));
-        HIP_CHECK(hipEventCreate(&e1));
-        std::vector<float> best(cand.size(), 1e30f);
-        const int warm = 8, timed = 4;
-        for (int round = 0; round < 2; ++round)
-            for (size_t c = 0; c < cand.size(); ++c) {
-                set_stream_lattices(s, cand[c][0], cand[c][1]);
-                for (int i = 0; i < (round == 0 && c == 0 ? warm : 1); ++i)
-                    HIP_CHECK(launch_stream2d(s.a3_int[i & 1], s.n3_int, spl, false, stream_cfg, s.s_comp));
-                HIP_CHECK(hipEventRecord(e0, s.s_comp));
-                for (int i = 0; i < timed; ++i)
-                    HIP_CHECK(launch_stream2d(s.a3_int[i & 1], s.n3_int, spl, false, stream_cfg, s.s_comp));
-                HIP_CHECK(hipEventRecord(e1, s.s_comp));
-                HIP_CHECK(hipEventSynchronize(e1));
-                float ms = 0.f;
-                HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-                best[c] = std::min(best[c], ms / timed);
-            }
-        HIP_CHECK(hipEventDestroy(e0));
-        HIP_CHECK(hipEventDestroy(e1));
         size_t keep = 0;
-        for (size_t c = 1; c < cand.size(); ++c)
-            if (best[c] < best[keep]) keep = c;
-        probe_ms.assign(best.begin(), best.end());
-        probe_kept = (int)keep;
-        if (getenv("LBM_PLACEMENT_LOG")) {
-            fprintf(stderr, "lbm placement probe (%dx%d): ms per launch", s.w, s.h);
-            for (float v : best) fprintf(stderr, " %.4f", v);
-            fprintf(stderr, "; kept pair %d\n", probe_kept);
+        // on any failure inside the probe: free every extra candidate and put the
+        // original pair back, so the handle owns exactly what it allocated
+        auto unwind = [&]() {
+            for (size_t c = 1; c < cand.size(); ++c)
+                if (c != keep)
+                    for (float *&p : cand[c])
+                        if (p) {
+                            (void)hipFree(p);
+                            p = nullptr;
+                        }
+        };
+        try {
+            for (int c = 1; c < tries; ++c) {
+                std::array<float *, 2> f{nullptr, nullptr};
+                if (hipMalloc(&f[0], sizeof(float) * n) != hipSuccess) { (void)hipGetLastError(); break; }
+                if (hipMalloc(&f[1], sizeof(float) * n) != hipSuccess) {
+                    (void)hipGetLastError();
+                    (void)hipFree(f[0]);
+                    break;
+                }
+                cand.push_back(f);
+            }
+            const unsigned fill = 0x3dcccccdu;  // 0.1f: rho = 0.9 everywhere, no tiny-density path
+            for (auto &f : cand)
+                for (float *p : f)
+                    HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), (int)fill, n, s.s_comp));
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            std::vector<float> best(cand.size(), 1e30f);
+            const int warm = 8, timed = 4;
+            for (int round = 0; round < 2; ++round)
+                for (size_t c = 0; c < cand.size(); ++c) {
+                    set_stream_lattices(s, cand[c][0], cand[c][1]);
+                    for (int i = 0; i < (round == 0 && c == 0 ? warm : 1); ++i)
+                        HIP_CHECK(launch_stream2d(s.a3_int[i & 1], s.n3_int, spl, false, stream_cfg, tolerance,
+                                                  s.s_comp));
+                    HIP_CHECK(hipEventRecord(e0, s.s_comp));
+                    for (int i = 0; i < timed; ++i)
+                        HIP_CHECK(launch_stream2d(s.a3_int[i & 1], s.n3_int, spl, false, stream_cfg, tolerance,
+                                                  s.s_comp));
+                    HIP_CHECK(hipEventRecord(e1, s.s_comp));
+                    HIP_CHECK(hipEventSynchronize(e1));
+                    float ms = 0.f;
+                    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+                    best[c] = std::min(best[c], ms / timed);
+                }
+            HIP_CHECK(hipEventDestroy(e0));
+            HIP_CHECK(hipEventDestroy(e1));
+            for (size_t c = 1; c < cand.size(); ++c)
+                if (best[c] < best[keep]) keep = c;
+            // LBM_PLACEMENT_KEEP=k (tests): keep candidate k whatever the timings,
+            // so the swap path (k > 0) is exercised deterministically
+            const int force = knob("LBM_PLACEMENT_KEEP", -1);
+            if (force >= 0 && force < (int)cand.size()) keep = (size_t)force;
+            probe_ms.assign(best.begin(), best.end());
+            probe_kept = (int)keep;
+            if (knob_str("LBM_PLACEMENT_LOG")) {
+                fprintf(stderr, "lbm placement probe (%dx%d): ms per launch", s.w, s.h);
+                for (float v : best) fprintf(stderr, " %.4f", v);
+                fprintf(stderr, "; kept pair %d\n", probe_kept);
+            }
+            unwind();
+            if (keep != 0)
+                for (float *&p : cand[0]) {
+                    float *q = p;
+                    p = nullptr;
+                    HIP_CHECK(hipFree(q));
+                }
+            set_stream_lattices(s, cand[keep][0], cand[keep][1]);
+            for (float *p : cand[keep]) fill_fresh(p, sizeof(float) * n, s.s_comp);
+            build_args(s);
+        } catch (...) {
+            // keep == 0 here unless the failure came after the choice; either way
+            // the handle ends up owning exactly one pair
+            unwind();
+            if (keep != 0 && cand[0][0]) {  // original pair not yet freed: fall back to it
+                for (float *&p : cand[keep])
+                    if (p) (void)hipFree(p);
+                keep = 0;
+            }
+            s.f[0] = cand[keep][0];
+            s.f[1] = cand[keep][1];
+            for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + s.origin_off;
+            throw;
         }
-        for (size_t c = 0; c < cand.size(); ++c)
-            if (c != keep)
-                for (float *p : cand[c]) HIP_CHECK(hipFree(p));
-        set_stream_lattices(s, cand[keep][0], cand[keep][1]);
-        for (float *p : cand[keep]) HIP_CHECK(hipMemset(p, 0, sizeof(float) * n));
-        build_args(s);
     }
 
     // `st` waits for the last exchange: own ghosts unpacked, and (LOCAL)
@@ -1424,7 +1511,7 @@ struct lbm_handle {
             if (n <= 0) return hipSuccess;
             const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
             if (stream_v == 1) return launch_stream(a, n, spl, interior, st);
-            if (stream_v == 3) return launch_stream2d(a, n, spl, interior, stream_cfg, st);
+            if (stream_v == 3) return launch_stream2d(a, n, spl, interior, stream_cfg, tolerance, st);
             return launch_stream2c(a, n, spl, interior, stream_waves, st);
         }
         if (fused_launch) {
@@ -1536,12 +1623,15 @@ struct lbm_handle {
         if (!loaded) throw lbm_failure(LBM_E_STATE, "lattice not initialised (call lbm_load_cells or lbm_init_equilibrium)");
         if (steps < 0) throw lbm_failure(LBM_E_INVALID, "steps must be >= 0");
         ensure_av(std::max(steps, 1));
+        run_fused = run_single = 0;
         if (resident) {
             run_resident(steps, accelerate_first);
+            run_fused = steps > 0 ? 1 : 0;
             return;
         }
         if (pipeline) {
             run_pipeline(steps);
+            run_single = steps;
             return;
         }
         for (auto &s : subs) {
@@ -1582,6 +1672,8 @@ struct lbm_handle {
         for (; l < launches; ++l) launch_once(fused);
         const int rem = steps - launches * per_launch;
         for (int i = 0; i < rem; ++i) launch_once(false);  // remainder: one-step kernel (W1 halo) ...
+        run_fused = fused ? launches : 0;
+        run_single = fused ? rem : launches;
         join();
         if (rem > 0) refresh_halos();                      // ... then restore the WG ring for the next launch
         for (auto &s : subs) {
@@ -1604,7 +1696,7 @@ struct lbm_handle {
     // LBM_STREAM_TRACE=<file>: raw {start, end} s_memrealtime (100 MHz) per
     // block of sub-domain 0's last interior stream launch (tools/stream_trace.py)
     void dump_trace() {
-        const char *path = getenv("LBM_STREAM_TRACE");
+        const char *path = knob_str("LBM_STREAM_TRACE");
         if (!path || !*path || subs.empty() || !subs[0].trace) return;
         Sub &s = subs[0];
         set_device(s);
@@ -1919,6 +2011,29 @@ int32_t lbm_kernel_in_use(lbm_handle *h) {
     if (h->fused) return h->use_stream ? LBM_KERNEL_STREAM : LBM_KERNEL_STEP2;
     return h->vec4 ? LBM_KERNEL_VEC4 : LBM_KERNEL_SCALAR;
 }
+
+int lbm_run_stats(lbm_handle *h, int32_t *fused_launches, int32_t *one_step_launches) {
+    if (!h) return LBM_E_INVALID;
+    if (fused_launches) *fused_launches = h->run_fused;
+    if (one_step_launches) *one_step_launches = h->run_single;
+    return LBM_OK;
+}
+
+int lbm_placement_probe(lbm_handle *h, int32_t *kept, int32_t *tried, float *ms_per_launch, int32_t max_ms) {
+    if (!h) return LBM_E_INVALID;
+    if (kept) *kept = h->probe_kept;
+    if (tried) *tried = (int32_t)h->probe_ms.size();
+    if (ms_per_launch)
+        for (int i = 0; i < (int)h->probe_ms.size() && i < max_ms; ++i) ms_per_launch[i] = h->probe_ms[i];
+    return LBM_OK;
+}
+
+int32_t lbm_numerics(lbm_handle *h) {
+    if (!h) return -1;
+    return (h->tolerance && h->use_stream && h->stream_v == 3 && h->fused && !h->resident && !h->pipeline) ? 1 : 0;
+}
+
+const char *lbm_source_hash(void) { return LBM_SOURCE_HASH; }
 
 int32_t lbm_steps_per_launch(lbm_handle *h) {
     if (!h) return 0;

@@ -156,6 +156,7 @@ struct StreamArgs {
     int w, h, xmax;         // xmax: last column inside the row allocation (>= w + gr + 1)
     int gy0, ny, accel_g;
     float omega, omo, w1, w2;
+    float tc0, tc1, tc2;    // LBM_FLAG_TOLERANCE collision: 4 omega / 9, omega / 9, omega / 36
     int nrect, total;       // total work units (strip x segment)
     SRect rect[MAX_SRECTS];
     int rect_begin[MAX_SRECTS];

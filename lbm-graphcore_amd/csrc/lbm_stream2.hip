@@ -286,8 +286,9 @@ __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2
 // OBST = false: the work unit reads no obstacle cell (stream2d_flags), so the
 // obstacle bytes are neither loaded nor tracked and no level carries the
 // rebound selects (their merge cost ~18 register copies per cell pair).
-template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST>
-__device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j) {
+template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL>
+__device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j,
+                                             const TolK &tk) {
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
     if (PD == 1) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
     if (OBST) {
@@ -325,7 +326,11 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         const bool any_obst = OBST && ((st.rob >> L) & 1ull);
         int gy = a.gy0 + y;
         gy = gy < 0 ? gy + a.ny : (gy >= a.ny ? gy - a.ny : gy);
-        const f2 usq = collide2u(s, o, oa, ob, any_obst, gy == a.accel_g, a.omega, a.omo, a.w1, a.w2);
+        f2 usq;
+        if constexpr (TOL)
+            usq = collide2t(s, o, oa, ob, any_obst, gy == a.accel_g, tk, a.w1, a.w2);
+        else
+            usq = collide2u(s, o, oa, ob, any_obst, gy == a.accel_g, a.omega, a.omo, a.w1, a.w2);
         const bool rowlive = (!GUARD || y >= g.yo0) && (L == S || y < g.yo1);
         if (rowlive) {
             const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
@@ -397,9 +402,10 @@ __device__ __forceinline__ Stream2Geo stream2d_geo(const StreamArgs &a, int t, i
 }
 
 // One work unit (strip x segment t) of the launch; accumulates |u| per level into st.tot.
-template <int S, int PD, bool NT, bool OBST>
+template <int S, int PD, bool NT, bool OBST, bool TOL>
 __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st) {
     const Stream2Geo g = stream2d_geo<S>(a, t, lane);
+    const TolK tk{a.omo, a.tc0, a.tc1, a.tc2};
 
 #pragma unroll
     for (int b = 0; b < S; ++b) {
@@ -414,15 +420,15 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     int j = g.j0;
 #pragma unroll 1
     for (int i = 0; i < S; ++i, j += 2) {
-        stream2d_row<S, 0, true, PD, NT, OBST>(a, g, st, j);
-        stream2d_row<S, 1, true, PD, NT, OBST>(a, g, st, j + 1);
+        stream2d_row<S, 0, true, PD, NT, OBST, TOL>(a, g, st, j, tk);
+        stream2d_row<S, 1, true, PD, NT, OBST, TOL>(a, g, st, j + 1, tk);
     }
 #pragma unroll 1
     for (; j + 1 <= g.jlast; j += 2) {
-        stream2d_row<S, 0, false, PD, NT, OBST>(a, g, st, j);
-        stream2d_row<S, 1, false, PD, NT, OBST>(a, g, st, j + 1);
+        stream2d_row<S, 0, false, PD, NT, OBST, TOL>(a, g, st, j, tk);
+        stream2d_row<S, 1, false, PD, NT, OBST, TOL>(a, g, st, j + 1, tk);
     }
-    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST>(a, g, st, j);
+    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL>(a, g, st, j, tk);
 }
 
 // |u| partials of one work unit, one per level (= time step of the launch)
@@ -449,7 +455,7 @@ __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, 
 // (A persistent grid taking units from a device-scope counter balanced the
 // waves better but read 1.30x the algorithmic bytes instead of 1.18x:
 // neighbouring strips landed on different XCDs.)
-template <int S, bool kReduce, int W, bool NT>
+template <int S, bool kReduce, int W, bool NT, bool TOL = false>
 __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     __shared__ float lds[W];
     if (kReduce && blockIdx.x == 0) reduce_pending_n<64 * W>(a.ctl, a.partials_prev, a.av_local, lds);
@@ -471,9 +477,9 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
         // read no obstacle cell run the select-free copy of the unit loop
         typedef const __attribute__((address_space(4))) uint8_t CU8;
         if (a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0)
-            stream2d_unit<S, 1, NT, true>(a, t, lane, st);
+            stream2d_unit<S, 1, NT, true, TOL>(a, t, lane, st);
         else
-            stream2d_unit<S, 1, NT, false>(a, t, lane, st);
+            stream2d_unit<S, 1, NT, false, TOL>(a, t, lane, st);
     }
     if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
@@ -514,18 +520,26 @@ hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, h
     return hipGetLastError();
 }
 
-template <int S, int W, bool NT>
+template <int S, int W, bool NT, bool TOL = false>
 static void launch_s2d(const StreamArgs &a, int units, bool reduce, hipStream_t s) {
     const int blocks = (units + W - 1) / W;
     if (reduce)
-        hipLaunchKernelGGL((stream_steps2d<S, true, W, NT>), dim3(blocks), dim3(64 * W), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, true, W, NT, TOL>), dim3(blocks), dim3(64 * W), 0, s, a);
     else
-        hipLaunchKernelGGL((stream_steps2d<S, false, W, NT>), dim3(blocks), dim3(64 * W), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, false, W, NT, TOL>), dim3(blocks), dim3(64 * W), 0, s, a);
 }
 
 // waves per CU of the configuration (cfg: 0 = one wave per workgroup, plain
 // stores; 1 = four waves, plain; 2 = four waves, nt stores; 3 = one wave, nt stores)
-hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n) {
+hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
+    if (tol) {
+        const void *ft = steps == 2   ? (const void *)&stream_steps2d<2, false, 1, false, true>
+                         : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false, true>
+                         : steps == 5 ? (const void *)&stream_steps2d<5, false, 1, false, true>
+                         : steps == 6 ? (const void *)&stream_steps2d<6, false, 1, false, true>
+                                      : (const void *)&stream_steps2d<4, false, 1, false, true>;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ft, 64, 0);
+    }
     const void *fn = steps == 2   ? (const void *)&stream_steps2d<2, false, 1, false>
                      : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false>
                      : steps == 5 ? (const void *)&stream_steps2d<5, false, 1, false>
@@ -535,7 +549,20 @@ hipError_t stream2d_blocks_per_cu(int steps, int cfg, int &n) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, 0);
 }
 
-hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, hipStream_t s) {
+// tol: the LBM_FLAG_TOLERANCE collision (collide2t), one wave per workgroup,
+// plain stores (the launch form is the default cfg 0 whatever cfg says)
+hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s) {
+    if (tol) {
+        switch (steps) {
+            case 2: launch_s2d<2, 1, false, true>(a, units, reduce, s); break;
+            case 3: launch_s2d<3, 1, false, true>(a, units, reduce, s); break;
+            case 4: launch_s2d<4, 1, false, true>(a, units, reduce, s); break;
+            case 5: launch_s2d<5, 1, false, true>(a, units, reduce, s); break;
+            case 6: launch_s2d<6, 1, false, true>(a, units, reduce, s); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (steps * 10 + cfg) {
         case 20: launch_s2d<2, 1, false>(a, units, reduce, s); break;
         case 30: launch_s2d<3, 1, false>(a, units, reduce, s); break;

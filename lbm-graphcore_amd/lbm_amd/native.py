@@ -19,13 +19,13 @@ PKG_ROOT = Path(__file__).resolve().parent.parent          # lbm-graphcore_amd/
 LIB_PATH = Path(os.environ.get("LBM_HIP_LIB", PKG_ROOT / "build" / "liblbm_hip.so"))
 
 Q = 9
-ABI_VERSION = 3          # LBM_ABI_VERSION in include/lbm_hip.h
+ABI_VERSION = 4          # LBM_ABI_VERSION in include/lbm_hip.h
 
 LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
 TRANSPORT_LOCAL, TRANSPORT_RCCL = 0, 1
 KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4, KERNEL_STEP2, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PIPELINE = range(7)
-FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP = 1, 2
+FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP, FLAG_TOLERANCE = 1, 2, 4
 
 # every symbol include/lbm_hip.h declares
 EXPORTED = [
@@ -34,6 +34,7 @@ EXPORTED = [
     "lbm_run", "lbm_run_steps", "lbm_store", "lbm_load_cells_local", "lbm_store_local", "lbm_local_cells",
     "lbm_last_run_seconds",
     "lbm_total_free_cells", "lbm_local_rects", "lbm_kernel_in_use", "lbm_steps_per_launch",
+    "lbm_run_stats", "lbm_placement_probe", "lbm_numerics", "lbm_source_hash",
     "lbm_last_error", "lbm_destroy",
 ]
 # every symbol include/lbm3d_hip.h declares (D3Q19 extension)
@@ -95,7 +96,11 @@ _lib = None
 
 
 def load_library() -> ctypes.CDLL:
-    """Load liblbm_hip.so and declare every C-ABI signature (no GPU needed)."""
+    """Load liblbm_hip.so and declare every C-ABI signature (no GPU needed).
+
+    Refuses a library whose compiled-in source hash (lbm_source_hash) differs
+    from the hash of the csrc/ and include/ sources beside it: a stale build
+    fails loudly instead of silently running old kernels."""
     global _lib
     if _lib is not None:
         return _lib
@@ -104,6 +109,13 @@ def load_library() -> ctypes.CDLL:
             f"{LIB_PATH} not found: build the HIP library first (make -C lbm-graphcore_amd "
             "or __graft_entry__.build()); there is no CPU fallback")
     L = ctypes.CDLL(str(LIB_PATH))
+    L.lbm_source_hash.argtypes = []
+    L.lbm_source_hash.restype = ctypes.c_char_p
+    built = L.lbm_source_hash().decode()
+    from . import srchash
+    if srchash.source_files() and built != srchash.source_hash():
+        raise RuntimeError(f"{LIB_PATH} was built from other sources (hash {built}, sources "
+                           f"{srchash.source_hash()}): rebuild it (make -C lbm-graphcore_amd)")
     H = ctypes.c_void_p
     i32, i64 = ctypes.c_int32, ctypes.c_int64
     f32p = ctypes.POINTER(ctypes.c_float)
@@ -130,6 +142,9 @@ def load_library() -> ctypes.CDLL:
         "lbm_local_rects": ([H, ctypes.POINTER(Rect), i32, i32p], ctypes.c_int),
         "lbm_kernel_in_use": ([H], i32),
         "lbm_steps_per_launch": ([H], i32),
+        "lbm_run_stats": ([H, i32p, i32p], ctypes.c_int),
+        "lbm_placement_probe": ([H, i32p, i32p, f32p, i32], ctypes.c_int),
+        "lbm_numerics": ([H], i32),
         "lbm_last_error": ([H], ctypes.c_char_p),
         "lbm_destroy": ([H], None),
         "lbm3d_create": ([ctypes.POINTER(Params3D), u8p, ctypes.POINTER(Config), ctypes.POINTER(H)], ctypes.c_int),
@@ -305,6 +320,23 @@ class Engine:
 
     def steps_per_launch(self) -> int:
         return int(self._L.lbm_steps_per_launch(self._h))
+
+    def run_stats(self):
+        """(fused launches, one-step launches) of the last run."""
+        a, b = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self._L.lbm_run_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def placement(self):
+        """(kept pair or -1, [ms per launch of each pair tried]) of the placement probe."""
+        kept, tried = ctypes.c_int32(), ctypes.c_int32()
+        ms = (ctypes.c_float * 16)()
+        self._check(self._L.lbm_placement_probe(self._h, ctypes.byref(kept), ctypes.byref(tried), ms, 16))
+        return kept.value, [ms[i] for i in range(min(tried.value, 16))]
+
+    def numerics(self) -> str:
+        """'bitwise' (every kernel equals the CPU oracle) or 'tolerance' (LBM_FLAG_TOLERANCE collision)."""
+        return "tolerance" if int(self._L.lbm_numerics(self._h)) == 1 else "bitwise"
 
     def close(self) -> None:
         if self._h:

@@ -9,6 +9,7 @@ from __future__ import annotations
 import gzip
 import io as _io
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -24,12 +25,18 @@ for p in (str(ROOT), str(PKG)):
 
 from lbm_amd import io as lio  # noqa: E402
 
+# The library reads its tuning knobs (LBM_STREAM_V, LBM_TILE2, ...) only with
+# LBM_DEBUG_KNOBS=1; the tests that select variants through them need it.
+# Unset knobs keep the product defaults.
+os.environ.setdefault("LBM_DEBUG_KNOBS", "1")
+
 GRIDS = ["128x128", "128x256", "256x256", "1024x1024"]
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD MI355X GPU (HIP path through the C ABI)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "multigpu: needs >= 2 GPUs (skipped otherwise)")
 
 
 def load_problem(grid: str, iters: int | None = None):

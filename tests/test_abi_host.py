@@ -50,7 +50,19 @@ def test_library_exports_every_declared_symbol():
                          check=True).stdout
     for s in syms:
         assert re.search(rf"\bT {s}\b", out), s
-    assert L.lbm_abi_version() == 3
+    assert L.lbm_abi_version() == 4
+
+
+def test_stale_library_is_refused(monkeypatch):
+    """The binding compares the library's compiled-in source hash with the
+    sources beside it and refuses a stale build (no silent old kernels)."""
+    from lbm_amd import srchash
+    L = native.load_library()
+    assert L.lbm_source_hash().decode() == srchash.source_hash()
+    monkeypatch.setattr(native, "_lib", None)
+    monkeypatch.setattr(srchash, "source_hash", lambda: "0000000000000000")
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        native.load_library()
 
 
 def test_no_torch_types_in_abi():

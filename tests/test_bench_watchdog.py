@@ -1,6 +1,7 @@
 """bench.py's aux watchdog (CPU): a hanging aux measurement must not cost the
 line -- past the budget rank 0 prints the line with the aux done so far and
-every rank exits 0; within the budget the line is printed exactly once."""
+every rank exits with bench.WATCHDOG_EXIT (3, so the launcher sees that an aux
+hung); within the budget the line is printed exactly once and the exit is 0."""
 from __future__ import annotations
 
 import json
@@ -27,7 +28,7 @@ def test_watchdog_prints_and_exits_on_hang():
                 'out["aux"]["done_before_hang"] = 1\n'
                 'time.sleep(30)\n'
                 'print("not reached")\n')
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == 3, p.stderr
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1 and "not reached" not in p.stdout
     d = json.loads(lines[0])
@@ -39,7 +40,7 @@ def test_watchdog_other_ranks_exit_silently():
     p, _ = run('out = {"metric": "m", "value": 1.0}\n'
                'w = bench.AuxWatchdog(0.5, out, 3)\n'
                'time.sleep(30)\n')
-    assert p.returncode == 0 and p.stdout.strip() == ""
+    assert p.returncode == 3 and p.stdout.strip() == ""
 
 
 def test_watchdog_finish_prints_once():

@@ -205,26 +205,44 @@ def test_determinism_and_rerun(gpu_lib):
     np.testing.assert_allclose(outs[0][1], av2, rtol=1e-4)
 
 
-@pytest.mark.parametrize("mode", ["step2", "stream4", "stream5"])
-def test_large_grid_steps_and_conservation(gpu_lib, mode):
-    """8192^2 (the roofline config): 4 steps bitwise vs oracle, then mass conserved over 200 steps."""
-    n = 8192
-    p = lio.Params(n, n, 4, 10, 0.1, 0.005, 1.85)
+def bench_obstacles(n):
+    """BASELINE config 3/4 synthetic obstacles (bench.py): box walls + column nx/3."""
     obst = np.zeros((n, n), np.uint8)
     obst[0, :] = obst[-1, :] = 1
     obst[:, 0] = obst[:, -1] = 1
     obst[:, n // 3] = 1
+    return obst
+
+
+@pytest.mark.parametrize("mode", ["step2", "stream4", "stream5", "auto"])
+def test_large_grid_steps_and_conservation(gpu_lib, mode):
+    """8192^2 (the roofline config, BASELINE config 3): 11 steps bitwise vs the
+    oracle -- for the headline kernel (auto = stream, S = 5, default guide
+    tiers, per-unit obstacle flags, XCD unit permutation, placement probe on)
+    that is two fused 5-step launches plus a one-step remainder, and the test
+    asserts the fused launches ran -- then mass conserved over 200 steps.
+    Reference work unit: LastChance.cpp:192-266."""
+    n = 8192
+    p = lio.Params(n, n, 11, 10, 0.1, 0.005, 1.85)
+    obst = bench_obstacles(n)
     cells0 = lio.init_cells(p)
-    ref, ref_av = oracle.run(p, obst, 4, cells0)
-    with gpu_lib.Engine(p, obst, **mode_kw(gpu_lib, mode)) as e:
-        assert e.kernel_in_use() == kname(mode)
+    ref, ref_av = oracle.run_mt(p, obst, 11, 16, cells0)
+    kw = {} if mode == "auto" else mode_kw(gpu_lib, mode)
+    with gpu_lib.Engine(p, obst, **kw) as e:
+        assert e.kernel_in_use() == ("stream" if mode == "auto" else kname(mode))
+        spl = e.steps_per_launch()
+        if mode in ("auto", "stream5"):
+            assert spl == 5
         e.init_equilibrium()
-        e.run_steps(4, accelerate_first=True)
-        cells, av = e.store(n_av=4)
+        e.run_steps(11, accelerate_first=True)
+        fused, single = e.run_stats()
+        assert (fused, single) == (11 // spl, 11 % spl) and fused >= 1
+        cells, av = e.store(n_av=11)
         assert np.array_equal(cells, ref)
         # the oracle sums 67M |u| terms sequentially in fp32 (~sqrt(n)*eps ~ 5e-4
         # relative drift); the GPU sums in trees
         np.testing.assert_allclose(av, ref_av, rtol=2e-3)
+        del ref
         m0 = np.sum(cells, dtype=np.float64)
         e.run_steps(200)
         cells2, av2 = e.store(n_av=200)
@@ -317,12 +335,31 @@ def test_stream_segments_bitwise(gpu_lib, version, S, hs, monkeypatch):
             np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
+def test_16384_single_domain_vs_oracle(gpu_lib):
+    """BASELINE config 4's grid on one GPU with the headline kernel (auto =
+    stream, S = 5, placement probe on): 6 steps = one fused 5-step launch +
+    one one-step launch, bitwise vs the oracle (OpenMP restatement, the same
+    lattice as oracle.run) over the full 16384^2 lattice."""
+    n = 16384
+    p = lio.Params(n, n, 6, 10, 0.1, 0.005, 1.85)
+    obst = bench_obstacles(n)
+    with gpu_lib.Engine(p, obst) as e:
+        assert e.kernel_in_use() == "stream" and e.steps_per_launch() == 5
+        e.init_equilibrium()
+        e.run_steps(6, accelerate_first=True)
+        assert e.run_stats() == (1, 1)
+        cells, av = e.store(n_av=6)
+    ref, ref_av = oracle.run_mt(p, obst, 6, 16, lio.init_cells(p))
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=5e-3)  # 268M-term sequential fp32 sums in the oracle
+
+
 def test_16384_lattice_64bit_indexing(gpu_lib):
     """BASELINE config 4's 16384^2 sub-domain holds 2.4e9 floats per lattice (over
     2^31): every index into it must be 64-bit.  (The one-step kernels' ghost-edge
     stores once formed y * pitch in 32 bits and faulted there -- reached by the
-    remainder of a step count that is not a multiple of the stream kernel's 4.)
-    6 steps = one 4-step stream launch + two one-step launches, against six
+    remainder of a step count that is not a multiple of the stream kernel's S.)
+    6 steps = one 5-step stream launch + one one-step launch, against six
     one-step (vec4) launches: bitwise equal and finite."""
     n = 16384
     p = lio.Params(n, n, 6, 10, 0.1, 0.005, 1.85)
@@ -701,15 +738,23 @@ def test_placement_probe_same_lattice(gpu_lib, transport, monkeypatch):
     obst[p.ny // 4: p.ny // 2, p.nx // 3] = 1
     cells0 = lio.init_cells(p)
     out = []
-    for tries in ("1", "3"):
+    # tries=3 with LBM_PLACEMENT_KEEP=2: the last candidate is kept whatever the
+    # timings, so the swap path (original pair freed, launch arguments rebuilt
+    # on the new lattices) runs every time
+    for tries, keep in (("1", "-1"), ("3", "2")):
         monkeypatch.setenv("LBM_PLACEMENT_TRIES", tries)
+        monkeypatch.setenv("LBM_PLACEMENT_KEEP", keep)
         kw = dict(devices=[0], kernel=gpu_lib.KERNEL_STREAM)
         if transport == "rccl":
             kw.update(transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1, unique_id=gpu_lib.rccl_unique_id(),
                       flags=gpu_lib.FLAG_FORCE_EXCHANGE)
-        cells, av, used = gpu_run(gpu_lib, p, obst, cells0, 11, **kw)
-        assert used == "stream"
-        out.append((cells, av))
+        with gpu_lib.Engine(p, obst, **kw) as e:
+            kept, ms = e.placement()
+            assert (kept, len(ms)) == ((-1, 0) if tries == "1" else (2, 3))
+            assert e.kernel_in_use() == "stream"
+            e.load_cells(cells0)
+            e.run_steps(11, accelerate_first=True)
+            out.append(e.store(n_av=11))
     assert np.array_equal(out[0][0], out[1][0])
     assert np.array_equal(out[0][1], out[1][1])
     assert np.isfinite(out[1][1]).all()
