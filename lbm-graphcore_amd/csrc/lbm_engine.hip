@@ -200,8 +200,9 @@ struct lbm_handle {
     int og = 4;              // ghost width of the obstacle map
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     int stream_waves = 2;    // LBM_STREAM_W: register target of the two-column kernel (waves per SIMD)
-    int stream_cfg = 0;      // LBM_STREAM_CFG (v3): 0 one wave per workgroup; 1 four waves (adjacent strips);
-                             // 2 four waves + non-temporal lattice stores; 3 one wave + non-temporal stores
+    int stream_cfg = 0;      // LBM_STREAM_CFG (v3 launch form, one wave per workgroup): 0 plain stores;
+                             // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 8)
+    int tol_s = 5, tol_cfg = 0;  // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
@@ -290,11 +291,14 @@ struct lbm_handle {
         fused = knob("LBM_TWO_STEP", fused ? 1 : 0) != 0;
         tile2 = std::min(std::max(knob("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
         xoff = std::max(MAX_GR, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
-        stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 6);
+        stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 8);
         stream_hs = std::max(0, knob("LBM_STREAM_HS", stream_hs));
         stream_v = std::min(std::max(knob("LBM_STREAM_V", stream_v), 1), 3);
         stream_waves = knob("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
-        stream_cfg = std::min(std::max(knob("LBM_STREAM_CFG", stream_cfg), 0), 3);
+        auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
+        stream_cfg = form(knob("LBM_STREAM_CFG", stream_cfg), stream_cfg);
+        tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
+        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 8);
         stream_min_cells = std::max(0, knob("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
             const char *g = knob_str("LBM_STREAM_GUIDE");
@@ -640,7 +644,7 @@ struct lbm_handle {
             if (!(so && atoi(so) == 0)) {
                 std::vector<uint8_t> fl((size_t)ni + nb);
                 HIP_CHECK(hipMemcpy(fl.data(), s.uobst, fl.size(), hipMemcpyDeviceToHost));
-                const int W = (stream_cfg == 0 || stream_cfg == 3) ? 1 : 4;
+                const int W = 1;  // one wave per workgroup in every launch form
                 std::vector<int> perm((size_t)ni + nb);
                 auto order = [&](int off, int n) {
                     const int blocks = (n + W - 1) / W, q = blocks / 8, r = blocks % 8;
@@ -853,10 +857,15 @@ struct lbm_handle {
         }
         // register-streaming kernel: S steps per launch, S-wide ghost ring;
         // every sub-domain at least S cells (2S across a decomposed dimension)
-        const int s_max = stream_v == 3 ? 6 : 4;  // the v3 kernel takes up to 6 steps per launch
-        const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch : std::min(stream_s, s_max);
+        // launch form: the tolerance collision has forms 0 and 4 only
+        if (tolerance && stream_v == 3) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
+        // the v3 kernel takes up to 6 steps per launch (8 in the LP form)
+        const int s_max = stream_v == 3 ? (stream_cfg == 4 ? 8 : 6) : 4;
+        const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch
+                                               : std::min(tolerance && stream_v == 3 ? tol_s : stream_s, s_max);
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max));
+        if (stream_v == 3 && stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5..8
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;

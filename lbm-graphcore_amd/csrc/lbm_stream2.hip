@@ -286,9 +286,15 @@ __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2
 // OBST = false: the work unit reads no obstacle cell (stream2d_flags), so the
 // obstacle bytes are neither loaded nor tracked and no level carries the
 // rebound selects (their merge cost ~18 register copies per cell pair).
-template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL>
+// LP (LDS planes): the older of the two rows of planes 2, 5, 6 a level keeps
+// (row y-1, read two row iterations after it was stored) lives in LDS
+// instead of registers -- lpl points at this lane's slot of a per-wave
+// [S][3][64] f2 array; each level reads row y-1 from it and writes row y
+// back (the same lane, the same address: no barrier, LDS keeps a wave's
+// order) -- 6 VGPRs fewer per level, so S = 6..8 fit without spills.
+template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL, bool LP>
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j,
-                                             const TolK &tk) {
+                                             const TolK &tk, f2 *lpl) {
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
     if (PD == 1) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
     if (OBST) {
@@ -311,11 +317,32 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         const int b = L - 1;
         const int y = j - L;
         // pulled populations of row y (level L-1 values; x +- 1 by DPP)
-        const f2 s[Q] = {st.c0[b],    st.c1[b],           st.p2[PAR][b],     st.c3[b], cur[4],
-                         st.p5[PAR][b], st.p6[PAR][b], right2(cur[7]), left2(cur[8])};
-        st.p2[PAR][b] = cur[2];
-        st.p5[PAR][b] = left2(cur[5]);
-        st.p6[PAR][b] = right2(cur[6]);
+        f2 s[Q];
+        if constexpr (LP) {
+            f2 *slot = lpl + b * 3 * 64;
+            s[2] = slot[0];
+            s[5] = slot[64];
+            s[6] = slot[128];
+            slot[0] = st.p2[0][b];
+            slot[64] = st.p5[0][b];
+            slot[128] = st.p6[0][b];
+            st.p2[0][b] = cur[2];
+            st.p5[0][b] = left2(cur[5]);
+            st.p6[0][b] = right2(cur[6]);
+        } else {
+            s[2] = st.p2[PAR][b];
+            s[5] = st.p5[PAR][b];
+            s[6] = st.p6[PAR][b];
+            st.p2[PAR][b] = cur[2];
+            st.p5[PAR][b] = left2(cur[5]);
+            st.p6[PAR][b] = right2(cur[6]);
+        }
+        s[0] = st.c0[b];
+        s[1] = st.c1[b];
+        s[3] = st.c3[b];
+        s[4] = cur[4];
+        s[7] = right2(cur[7]);
+        s[8] = left2(cur[8]);
         st.c0[b] = cur[0];
         st.c1[b] = left2(cur[1]);
         st.c3[b] = right2(cur[3]);
@@ -371,6 +398,9 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
 #pragma unroll
             for (int k = 0; k < Q; ++k) cur[k] = o[k];
         }
+        // LP forms: one level at a time (the scheduler would otherwise start
+        // the next level's LDS reads and shifts early and spill at S >= 6)
+        if constexpr (LP) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -402,10 +432,14 @@ __device__ __forceinline__ Stream2Geo stream2d_geo(const StreamArgs &a, int t, i
 }
 
 // One work unit (strip x segment t) of the launch; accumulates |u| per level into st.tot.
-template <int S, int PD, bool NT, bool OBST, bool TOL>
-__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st) {
+template <int S, int PD, bool NT, bool OBST, bool TOL, bool LP>
+__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st, f2 *lpl) {
     const Stream2Geo g = stream2d_geo<S>(a, t, lane);
     const TolK tk{a.omo, a.tc0, a.tc1, a.tc2};
+    if constexpr (LP) {
+#pragma unroll
+        for (int i = 0; i < 3 * S; ++i) lpl[i * 64] = mk2(0.f);
+    }
 
 #pragma unroll
     for (int b = 0; b < S; ++b) {
@@ -420,15 +454,15 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     int j = g.j0;
 #pragma unroll 1
     for (int i = 0; i < S; ++i, j += 2) {
-        stream2d_row<S, 0, true, PD, NT, OBST, TOL>(a, g, st, j, tk);
-        stream2d_row<S, 1, true, PD, NT, OBST, TOL>(a, g, st, j + 1, tk);
+        stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
+        stream2d_row<S, 1, true, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl);
     }
 #pragma unroll 1
     for (; j + 1 <= g.jlast; j += 2) {
-        stream2d_row<S, 0, false, PD, NT, OBST, TOL>(a, g, st, j, tk);
-        stream2d_row<S, 1, false, PD, NT, OBST, TOL>(a, g, st, j + 1, tk);
+        stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
+        stream2d_row<S, 1, false, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl);
     }
-    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL>(a, g, st, j, tk);
+    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
 }
 
 // |u| partials of one work unit, one per level (= time step of the launch)
@@ -455,9 +489,10 @@ __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, 
 // (A persistent grid taking units from a device-scope counter balanced the
 // waves better but read 1.30x the algorithmic bytes instead of 1.18x:
 // neighbouring strips landed on different XCDs.)
-template <int S, bool kReduce, int W, bool NT, bool TOL = false>
+template <int S, bool kReduce, int W, bool NT, bool TOL = false, bool LP = false>
 __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     __shared__ float lds[W];
+    __shared__ f2 lds_p[LP ? W * 3 * S * 64 : 1];  // LP: [wave][S][3][64]
     if (kReduce && blockIdx.x == 0) reduce_pending_n<64 * W>(a.ctl, a.partials_prev, a.av_local, lds);
 
     const int lane = threadIdx.x & 63;
@@ -477,9 +512,9 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
         // read no obstacle cell run the select-free copy of the unit loop
         typedef const __attribute__((address_space(4))) uint8_t CU8;
         if (a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0)
-            stream2d_unit<S, 1, NT, true, TOL>(a, t, lane, st);
+            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lds_p + (LP ? (threadIdx.x >> 6) * 3 * S * 64 : 0) + lane);
         else
-            stream2d_unit<S, 1, NT, false, TOL>(a, t, lane, st);
+            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lds_p + (LP ? (threadIdx.x >> 6) * 3 * S * 64 : 0) + lane);
     }
     if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
@@ -515,75 +550,100 @@ hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, h
         case 4: hipLaunchKernelGGL(stream2d_flags<4>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 5: hipLaunchKernelGGL(stream2d_flags<5>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 6: hipLaunchKernelGGL(stream2d_flags<6>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 7: hipLaunchKernelGGL(stream2d_flags<7>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 8: hipLaunchKernelGGL(stream2d_flags<8>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-template <int S, int W, bool NT, bool TOL = false>
+template <int S, bool NT, bool TOL = false, bool LP = false>
 static void launch_s2d(const StreamArgs &a, int units, bool reduce, hipStream_t s) {
-    const int blocks = (units + W - 1) / W;
     if (reduce)
-        hipLaunchKernelGGL((stream_steps2d<S, true, W, NT, TOL>), dim3(blocks), dim3(64 * W), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, true, 1, NT, TOL, LP>), dim3(units), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((stream_steps2d<S, false, W, NT, TOL>), dim3(blocks), dim3(64 * W), 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, false, 1, NT, TOL, LP>), dim3(units), dim3(64), 0, s, a);
 }
 
-// waves per CU of the configuration (cfg: 0 = one wave per workgroup, plain
-// stores; 1 = four waves, plain; 2 = four waves, nt stores; 3 = one wave, nt stores)
+template <int S, bool TOL, bool LP>
+static const void *s2d_fn() {
+    return (const void *)&stream_steps2d<S, false, 1, false, TOL, LP>;
+}
+
+// Launch forms (cfg; one wave per workgroup in all of them -- four-wave
+// workgroups on adjacent strips lost their A/B, profiles/r02/ab_cfg_s5.log):
+//   0 plain stores (default), 3 non-temporal lattice stores, 4 LP (older
+//   rows of planes 2, 5, 6 in LDS; S = 5..8).
+// tol: the LBM_FLAG_TOLERANCE collision (collide2t) in forms 0 and 4.
+static bool s2d_form_ok(int steps, int cfg, bool tol) {
+    if (cfg == 4) return steps >= 5 && steps <= 8;
+    if (cfg == 0) return steps >= 2 && steps <= 6;
+    if (cfg == 3) return !tol && steps >= 2 && steps <= 6;
+    return false;
+}
+
+// resident one-wave workgroups per CU of the instantiation a launch with
+// these parameters uses (the engine sizes segments to whole rounds of them)
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
-    if (tol) {
-        const void *ft = steps == 2   ? (const void *)&stream_steps2d<2, false, 1, false, true>
-                         : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false, true>
-                         : steps == 5 ? (const void *)&stream_steps2d<5, false, 1, false, true>
-                         : steps == 6 ? (const void *)&stream_steps2d<6, false, 1, false, true>
-                                      : (const void *)&stream_steps2d<4, false, 1, false, true>;
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ft, 64, 0);
+    if (!s2d_form_ok(steps, cfg, tol)) return hipErrorInvalidValue;
+    const void *fn = nullptr;
+    if (cfg == 4) {
+        switch (steps) {
+            case 5: fn = tol ? s2d_fn<5, true, true>() : s2d_fn<5, false, true>(); break;
+            case 6: fn = tol ? s2d_fn<6, true, true>() : s2d_fn<6, false, true>(); break;
+            case 7: fn = tol ? s2d_fn<7, true, true>() : s2d_fn<7, false, true>(); break;
+            default: fn = tol ? s2d_fn<8, true, true>() : s2d_fn<8, false, true>(); break;
+        }
+    } else {  // cfg 3 has the registers of cfg 0
+        switch (steps) {
+            case 2: fn = tol ? s2d_fn<2, true, false>() : s2d_fn<2, false, false>(); break;
+            case 3: fn = tol ? s2d_fn<3, true, false>() : s2d_fn<3, false, false>(); break;
+            case 4: fn = tol ? s2d_fn<4, true, false>() : s2d_fn<4, false, false>(); break;
+            case 5: fn = tol ? s2d_fn<5, true, false>() : s2d_fn<5, false, false>(); break;
+            default: fn = tol ? s2d_fn<6, true, false>() : s2d_fn<6, false, false>(); break;
+        }
     }
-    const void *fn = steps == 2   ? (const void *)&stream_steps2d<2, false, 1, false>
-                     : steps == 3 ? (const void *)&stream_steps2d<3, false, 1, false>
-                     : steps == 5 ? (const void *)&stream_steps2d<5, false, 1, false>
-                     : steps == 6 ? (const void *)&stream_steps2d<6, false, 1, false>
-                                  : (const void *)&stream_steps2d<4, false, 1, false>;
-    (void)cfg;  // same registers per wave in every configuration: count waves of the one-wave form
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, 0);
 }
 
-// tol: the LBM_FLAG_TOLERANCE collision (collide2t), one wave per workgroup,
-// plain stores (the launch form is the default cfg 0 whatever cfg says)
 hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s) {
+    if (!s2d_form_ok(steps, cfg, tol)) return hipErrorInvalidValue;
+    if (cfg == 4) {
+        switch (steps * 2 + (tol ? 1 : 0)) {
+            case 10: launch_s2d<5, false, false, true>(a, units, reduce, s); break;
+            case 11: launch_s2d<5, false, true, true>(a, units, reduce, s); break;
+            case 12: launch_s2d<6, false, false, true>(a, units, reduce, s); break;
+            case 13: launch_s2d<6, false, true, true>(a, units, reduce, s); break;
+            case 14: launch_s2d<7, false, false, true>(a, units, reduce, s); break;
+            case 15: launch_s2d<7, false, true, true>(a, units, reduce, s); break;
+            case 16: launch_s2d<8, false, false, true>(a, units, reduce, s); break;
+            case 17: launch_s2d<8, false, true, true>(a, units, reduce, s); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (tol) {
         switch (steps) {
-            case 2: launch_s2d<2, 1, false, true>(a, units, reduce, s); break;
-            case 3: launch_s2d<3, 1, false, true>(a, units, reduce, s); break;
-            case 4: launch_s2d<4, 1, false, true>(a, units, reduce, s); break;
-            case 5: launch_s2d<5, 1, false, true>(a, units, reduce, s); break;
-            case 6: launch_s2d<6, 1, false, true>(a, units, reduce, s); break;
+            case 2: launch_s2d<2, false, true>(a, units, reduce, s); break;
+            case 3: launch_s2d<3, false, true>(a, units, reduce, s); break;
+            case 4: launch_s2d<4, false, true>(a, units, reduce, s); break;
+            case 5: launch_s2d<5, false, true>(a, units, reduce, s); break;
+            case 6: launch_s2d<6, false, true>(a, units, reduce, s); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
     switch (steps * 10 + cfg) {
-        case 20: launch_s2d<2, 1, false>(a, units, reduce, s); break;
-        case 30: launch_s2d<3, 1, false>(a, units, reduce, s); break;
-        case 40: launch_s2d<4, 1, false>(a, units, reduce, s); break;
-        case 21: launch_s2d<2, 4, false>(a, units, reduce, s); break;
-        case 31: launch_s2d<3, 4, false>(a, units, reduce, s); break;
-        case 41: launch_s2d<4, 4, false>(a, units, reduce, s); break;
-        case 22: launch_s2d<2, 4, true>(a, units, reduce, s); break;
-        case 32: launch_s2d<3, 4, true>(a, units, reduce, s); break;
-        case 42: launch_s2d<4, 4, true>(a, units, reduce, s); break;
-        case 50: launch_s2d<5, 1, false>(a, units, reduce, s); break;
-        case 51: launch_s2d<5, 4, false>(a, units, reduce, s); break;
-        case 52: launch_s2d<5, 4, true>(a, units, reduce, s); break;
-        case 23: launch_s2d<2, 1, true>(a, units, reduce, s); break;
-        case 33: launch_s2d<3, 1, true>(a, units, reduce, s); break;
-        case 43: launch_s2d<4, 1, true>(a, units, reduce, s); break;
-        case 53: launch_s2d<5, 1, true>(a, units, reduce, s); break;
-        case 63: launch_s2d<6, 1, true>(a, units, reduce, s); break;
-        case 60: launch_s2d<6, 1, false>(a, units, reduce, s); break;
-        case 61: launch_s2d<6, 4, false>(a, units, reduce, s); break;
-        case 62: launch_s2d<6, 4, true>(a, units, reduce, s); break;
+        case 20: launch_s2d<2, false>(a, units, reduce, s); break;
+        case 30: launch_s2d<3, false>(a, units, reduce, s); break;
+        case 40: launch_s2d<4, false>(a, units, reduce, s); break;
+        case 50: launch_s2d<5, false>(a, units, reduce, s); break;
+        case 60: launch_s2d<6, false>(a, units, reduce, s); break;
+        case 23: launch_s2d<2, true>(a, units, reduce, s); break;
+        case 33: launch_s2d<3, true>(a, units, reduce, s); break;
+        case 43: launch_s2d<4, true>(a, units, reduce, s); break;
+        case 53: launch_s2d<5, true>(a, units, reduce, s); break;
+        case 63: launch_s2d<6, true>(a, units, reduce, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -63,8 +63,10 @@ def main():
         for name, env in variants:
             for k in [k for k in os.environ if k.startswith("LBM_")]:
                 os.environ.pop(k, None)
-            os.environ.update(env)
-            with native.Engine(p, obst, devices=[0]) as e:
+            os.environ.update({k: v for k, v in env.items() if k.startswith("LBM")})
+            os.environ["LBM_DEBUG_KNOBS"] = "1"  # the library reads its knobs only with this set
+            flags = int(env.get("FLAGS", "0"))    # e.g. FLAGS=4: LBM_FLAG_TOLERANCE
+            with native.Engine(p, obst, devices=[0], flags=flags) as e:
                 e.init_equilibrium()
                 e.run_steps(a.warmup, accelerate_first=True)
                 e.run_steps(a.steps)
