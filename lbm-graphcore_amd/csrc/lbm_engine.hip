@@ -44,9 +44,6 @@
 namespace lbm {
 hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hipStream_t s);
 hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t s);
-hipError_t launch_stream(const StreamArgs &a, int blocks, int steps, bool reduce, hipStream_t s);
-hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s);
-hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n);
 hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s);
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n);
 hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, hipStream_t s);
@@ -195,11 +192,8 @@ struct lbm_handle {
     int gr = 2;              // ghost ring width
     int stream_s = 5;        // LBM_STREAM_S: steps per stream launch when not configured (v1 / v2 kernels: at most 4)
     int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
-    int stream_v = 3;        // LBM_STREAM_V: 1 = one column per lane, 2 = two columns per lane (packed fp32),
-                             // 3 = two columns per lane without the streaming order's redundant work
     int og = 4;              // ghost width of the obstacle map
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
-    int stream_waves = 2;    // LBM_STREAM_W: register target of the two-column kernel (waves per SIMD)
     int stream_cfg = 0;      // LBM_STREAM_CFG (v3 launch form, one wave per workgroup): 0 plain stores;
                              // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 8)
     int tol_s = 5, tol_cfg = 0;  // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
@@ -213,7 +207,7 @@ struct lbm_handle {
     int res_th_env = 0;
     int res_per_cu = 1;      // LBM_RES_PER_CU: tiles per CU the choice may plan for (1 or 2)
     int res_early_poll = 0;  // LBM_RES_EARLY: v2 polls the ring after its first work item
-    int res_version = 0;     // LBM_RES_V: 1 scalar 64-col tiles, 2 packed 128-col, 3 register-resident, 4 AA LDS; 0 = by grid
+    int res_version = 0;     // LBM_RES_V: 1 scalar 64-col tiles, 2 packed 128-col; 0 = by grid
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
     float *res_partials = nullptr;
@@ -293,8 +287,6 @@ struct lbm_handle {
         xoff = std::max(MAX_GR, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
         stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 8);
         stream_hs = std::max(0, knob("LBM_STREAM_HS", stream_hs));
-        stream_v = std::min(std::max(knob("LBM_STREAM_V", stream_v), 1), 3);
-        stream_waves = knob("LBM_STREAM_W", stream_waves) >= 3 ? 3 : 2;
         auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
         stream_cfg = form(knob("LBM_STREAM_CFG", stream_cfg), stream_cfg);
         tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
@@ -626,7 +618,7 @@ struct lbm_handle {
         // v3: which work units read an obstacle cell (the rest run without
         // rebound selects); obstacles and the work split are fixed from here on
         const char *uo = knob_str("LBM_STREAM_UOBST");
-        if (use_stream && stream_v == 3 && !(uo && atoi(uo) == 0)) {
+        if (use_stream && !(uo && atoi(uo) == 0)) {
             if (s.uobst) HIP_CHECK(hipFree(s.uobst));
             const int ni = std::max(0, s.a3_int[0].total), nb = std::max(0, s.a3_bnd[0].total);
             HIP_CHECK(hipMalloc(&s.uobst, (size_t)ni + nb + 1));
@@ -680,13 +672,13 @@ struct lbm_handle {
         // owned columns per strip: 64 - 2S (one column per lane); 128 - 2S
         // (two per lane), 2 fewer when the strip's first cell minus S is odd
         // (float2 alignment shifts the wave one column left)
-        auto ow_of = [&](int rx) { return stream_v == 1 ? 64 - 2 * S : (((rx - S) & 1) ? 126 - 2 * S : 128 - 2 * S); };
+        auto ow_of = [&](int rx) { return ((rx - S) & 1) ? 126 - 2 * S : 128 - 2 * S; };
         const bool xdec = s.remote[DE] || s.remote[DW];
         const bool ydec = s.remote[DN] || s.remote[DS];
         // a decomposed x side's boundary band is one whole strip wide when the
         // sub-domain has room: an S-column band costs nearly a full strip per
         // segment for S useful columns (tools/ab_parts.py)
-        const int ow_min = stream_v == 1 ? 64 - 2 * S : 126 - 2 * S;
+        const int ow_min = 126 - 2 * S;
         const int xb = (xdec && s.w >= 4 * ow_min) ? ow_min : b;
         const int y0 = ydec ? b : 0, y1 = ydec ? s.h - b : s.h;
         const int x0 = xdec ? xb : 0, x1 = xdec ? s.w - xb : s.w;
@@ -702,9 +694,8 @@ struct lbm_handle {
             // (profiles/r01/stream/ab_hs_rounds.log).  Eight rounds where the
             // segments stay at least 4S rows high, fewer otherwise.
             int per_cu = 0, cus = 0;
-            const hipError_t occ = stream_v == 3 ? stream2d_blocks_per_cu(S, stream_cfg, tolerance, per_cu)
-                                                 : stream2c_blocks_per_cu(S, stream_waves, per_cu);
-            if (stream_v >= 2 && occ == hipSuccess &&
+            const hipError_t occ = stream2d_blocks_per_cu(S, stream_cfg, tolerance, per_cu);
+            if (occ == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev) == hipSuccess &&
                 per_cu > 0 && cus > 0) {
                 const long long cap = (long long)per_cu * cus;
@@ -749,7 +740,7 @@ struct lbm_handle {
     // band's rows; the last tier takes the rest), "0" = uniform heights.
     template <class MK>
     bool guided_rects(int x0, int y0, int w, int h, MK &&mk, std::vector<SRect> &out) const {
-        if (stream_hs > 0 || stream_v != 3 || guide.empty()) return false;
+        if (stream_hs > 0 || guide.empty()) return false;
         constexpr int NB = 8;
         const int hb = h / NB;
         if (hb < 2 * guide[0].first) return false;
@@ -858,14 +849,14 @@ struct lbm_handle {
         // register-streaming kernel: S steps per launch, S-wide ghost ring;
         // every sub-domain at least S cells (2S across a decomposed dimension)
         // launch form: the tolerance collision has forms 0 and 4 only
-        if (tolerance && stream_v == 3) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
+        if (tolerance) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
         // the v3 kernel takes up to 6 steps per launch (8 in the LP form)
-        const int s_max = stream_v == 3 ? (stream_cfg == 4 ? 8 : 6) : 4;
+        const int s_max = stream_cfg == 4 ? 8 : 6;
         const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch
-                                               : std::min(tolerance && stream_v == 3 ? tol_s : stream_s, s_max);
+                                               : std::min(tolerance ? tol_s : stream_s, s_max);
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max));
-        if (stream_v == 3 && stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5..8
+        if (stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5..8
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;
@@ -982,20 +973,12 @@ struct lbm_handle {
         // (smallest tile height with one tile per CU first, except that 2-row
         // tiles are slower than 4-row ones on every grid measured:
         // profiles/r01/resident/)
-        // v3 (register-resident) only on request: with every wave owning full
-        // rows, the west / east edge populations are finished at the END of the
-        // collision phase and the hop to the neighbours is exposed -- 6.3 us per
-        // step at 1024^2 against 4.8 for v2's boundary-first schedule
-        // (profiles/r01/resident/ab_v2_v3.log, trace_v3.log)
-        if (p.nx % 128 == 0 && res_version == 3) order = {RES3_4, RES3_8, RES3_16, RES3_32, RES3_32x8, RES3_2};
-        if (p.nx % 2 == 0 && res_version == 4) order = {RES4_4, RES4_8, RES4_16, RES4_32, RES4_2, RES4_16x8};
         if (p.nx % 2 == 0 && (res_version == 0 || res_version == 2))
             order.insert(order.end(), {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2, RES2_16x8});
         if (res_version == 0 || res_version == 1) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});
         res_variant = -1;
         for (int v : order) {
             if (res_th_env > 0 && RES_TH[v] != res_th_env) continue;
-            if (RES_VER[v] == 3 && p.ny % RES_TH[v] != 0) continue;  // v3: exact tilings only
             const int tx = (p.nx + RES_TWV[v] - 1) / RES_TWV[v];
             const int ty = (p.ny + RES_TH[v] - 1) / RES_TH[v];
             int cap = 0;
@@ -1383,7 +1366,7 @@ struct lbm_handle {
         // five at 8192^2 (4.9 GB per pair), four at 16384^2 (19.5 GB)
         const int cap = (int)std::max<size_t>(1, (96ull << 30) / pair_bytes);
         const int tries = std::min({std::max(knob("LBM_PLACEMENT_TRIES", 5), 1), 8, cap});
-        if (tries <= 1 || !use_stream || stream_v != 3 || subs.size() != 1 || s.f_joint ||
+        if (tries <= 1 || !use_stream || subs.size() != 1 || s.f_joint ||
             (long long)s.w * s.h < (1LL << 25) || s.n3_int <= 0)
             return;
         const size_t n = (size_t)s.lattice_floats;
@@ -1519,9 +1502,7 @@ struct lbm_handle {
             const int n = interior ? s.n3_int : s.n3_bnd;
             if (n <= 0) return hipSuccess;
             const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
-            if (stream_v == 1) return launch_stream(a, n, spl, interior, st);
-            if (stream_v == 3) return launch_stream2d(a, n, spl, interior, stream_cfg, tolerance, st);
-            return launch_stream2c(a, n, spl, interior, stream_waves, st);
+            return launch_stream2d(a, n, spl, interior, stream_cfg, tolerance, st);
         }
         if (fused_launch) {
             const int n = interior ? s.n2_int : s.n2_bnd;
@@ -2039,7 +2020,7 @@ int lbm_placement_probe(lbm_handle *h, int32_t *kept, int32_t *tried, float *ms_
 
 int32_t lbm_numerics(lbm_handle *h) {
     if (!h) return -1;
-    return (h->tolerance && h->use_stream && h->stream_v == 3 && h->fused && !h->resident && !h->pipeline) ? 1 : 0;
+    return (h->tolerance && h->use_stream && h->fused && !h->resident && !h->pipeline) ? 1 : 0;
 }
 
 const char *lbm_source_hash(void) { return LBM_SOURCE_HASH; }

@@ -42,13 +42,13 @@ constexpr int MAX_SRECTS = 32;  // stream kernels: guided per-XCD row bands (lbm
 // fused two-step tile shapes (cells).  v1 (step2): LDS intermediate
 // 9 x (TH+2) x (TW+2) floats, 256 threads.  v2 (step2w): one wave per tile
 // row, TW = 64, planes 0/1/3 in registers, LDS 6 x (TH+2) x 66 floats.
-enum Tile2 : int {
-    T2_64x16 = 0, T2_64x8 = 1, T2_128x8 = 2, T2_32x16 = 3, T2_64x24 = 4,
-    T2V_64x16_W8 = 5, T2V_64x8_W8 = 6, T2V_64x16_W4 = 7, T2V_64x8_W4 = 8, T2V_64x32_W8 = 9
-};
-constexpr int NUM_TILE2 = 10;
-constexpr int T2_W[NUM_TILE2] = {64, 64, 128, 32, 64, 64, 64, 64, 64, 64};
-constexpr int T2_H[NUM_TILE2] = {16, 8, 8, 16, 24, 16, 8, 16, 8, 32};
+// The two shapes that won their A/B (profiles/r01/ab_step2_tiles.log): v2
+// 64x8 with 8 waves while the lattice pair lives in the Infinity Cache, v1
+// 64x8 once it streams from HBM (the other eight shapes were removed).
+enum Tile2 : int { T2_64x8 = 0, T2V_64x8_W8 = 1 };
+constexpr int NUM_TILE2 = 2;
+constexpr int T2_W[NUM_TILE2] = {64, 64};
+constexpr int T2_H[NUM_TILE2] = {8, 8};
 
 enum Dir : int { DE = 0, DN = 1, DW = 2, DS = 3, DNE = 4, DNW = 5, DSW = 6, DSE = 7 };
 
@@ -180,20 +180,17 @@ struct StreamArgs {
 // fp32, a column pair per lane): 128-column tiles, even nx only.
 constexpr int RES_TW = 64;
 constexpr int RES2_TW = 128;
-// v3 (register-resident, packed pairs): exact 128 x TH tilings only.
+// (v3, register-resident, and v4, AA-pattern LDS addressing, lost their A/B
+// to v2 -- DESIGN.md section 4 -- and were removed in round 3.)
 enum ResVariant : int {
     RES_64 = 0, RES_32 = 1, RES_16 = 2, RES_16x4 = 3, RES_8 = 4, RES_4 = 5,           // v1
     RES2_32 = 6, RES2_16 = 7, RES2_8 = 8, RES2_4 = 9, RES2_2 = 10,                    // v2
-    RES3_32 = 11, RES3_32x8 = 12, RES3_16 = 13, RES3_8 = 14, RES3_4 = 15, RES3_2 = 16,  // v3
-    RES2_16x8 = 17,                                                                     // v2, 8 waves: 2 tiles per CU
-    RES4_32 = 18, RES4_16 = 19, RES4_8 = 20, RES4_4 = 21, RES4_2 = 22,                 // v4: v2 tiles, AA pattern
-    RES4_16x8 = 23                                                                      // v4, 8 waves: 2 tiles per CU
+    RES2_16x8 = 11                                                                      // v2, 8 waves: 2 tiles per CU
 };
-constexpr int NUM_RES = 24;
-constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 32, 32, 16, 8, 4, 2, 16, 32, 16, 8, 4, 2, 16};
-constexpr int RES_TWV[NUM_RES] = {64,  64,  64,  64,  64,  64,  128, 128, 128, 128, 128, 128,
-                                  128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128};
-constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 2, 4, 4, 4, 4, 4, 4};
+constexpr int NUM_RES = 12;
+constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 16};
+constexpr int RES_TWV[NUM_RES] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128, 128};
+constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2};
 constexpr int RES_GW = 128;  // granule positions per (tile, direction, plane), both versions
 
 struct ResidentArgs {

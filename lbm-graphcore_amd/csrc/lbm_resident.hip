@@ -42,8 +42,6 @@
 // partials[t][tile]; resident_reduce folds the tiles in a fixed order into
 // av_local[t] after the launch.
 
-#include <type_traits>
-
 #include "lbm_packed.hpp"
 
 namespace lbm {
@@ -314,26 +312,8 @@ __global__ __launch_bounds__(64 * NW) void resident_steps(ResidentArgs a) {
 // LDS rows hold 132 floats (ring column at x = -1 and x = tw, pairs 8-byte
 // aligned): the unshifted pulls (N, S) are one ds_read_b64, the shifted ones
 // one ds_read2_b32, every write-back one ds_write_b64.
-//
-// v4 = v2 with AA-pattern LDS addressing (AA = true): the tile keeps ONE copy
-// of populations 1..8 and alternates two representations, so that within a
-// step every LDS slot is read and then written by the same cell and the
-// barrier between pull and write-back disappears (one barrier per step; a
-// wave's LDS reads overlap other waves' collisions):
-//   even step: s_k = F[k][x]            -> o_k into F[opp k][x]       (local)
-//   odd step:  s_k = F[opp k][x - c_k]  -> o_k into F[k][x + c_k]     (pull, push)
-// Slot (y, j) is touched in an odd step only by cell y - c_j, so a tile's
-// ring slots are its own edge cells' targets.  The ring is filled after an
-// even step (neighbours' o_k -> F[opp k][ring]); after an odd step the
-// neighbours' pushed o_k land directly in this tile's edge slots
-// F[k][ring + c_k].  Same granules, same publish sets as v2; the lattice
-// enters as pulled populations and leaves as post-collision ones.
 // ---------------------------------------------------------------------------
-__device__ constexpr int res_cx(int k) { return (k == 1 || k == 5 || k == 8) ? 1 : (k == 3 || k == 6 || k == 7) ? -1 : 0; }
-__device__ constexpr int res_cy(int k) { return (k == 2 || k == 5 || k == 6) ? 1 : (k == 4 || k == 7 || k == 8) ? -1 : 0; }
-__device__ constexpr int res_opp(int k) { return k == 0 ? 0 : k <= 4 ? (k + 1) % 4 + 1 : (k - 3) % 4 + 5; }
-
-template <int NW, int TH, int MINW = 1, bool AA = false>
+template <int NW, int TH, int MINW = 1>
 __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a) {
     constexpr int NT = 64 * NW;
     constexpr int LS = RES2_TW + 4;
@@ -367,8 +347,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             L[LJ(k, ly, (lx) + 1)] = (v).y;                      \
         }                                                        \
     } while (0)
-    auto wrapx = [&](int x) { return x < 0 ? x + a.nx : x >= a.nx ? x - a.nx : x; };
-    auto wrapy = [&](int y) { return y < 0 ? y + a.ny : y >= a.ny ? y - a.ny : y; };
     if (threadIdx.x == 0) abort_flag = 0;
 
     // ---- work items: boundary first ----------------------------------------
@@ -408,19 +386,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             const int gx = gx0 + 2 * px, gy = gy0 + ly;
             const float *src = a.fin + (long long)gy * pitch + gx;
             f0[it] = *reinterpret_cast<const f2 *>(src);
-            if constexpr (AA) {  // pulled populations: F[k][x] = f_k(x - c_k)
 #pragma unroll
-                for (int k = 1; k < Q; ++k) {
-                    const float *row = a.fin + k * P + (long long)wrapy(gy - res_cy(k)) * pitch;
-                    const f2 v = res_cx(k) == 0 ? *reinterpret_cast<const f2 *>(row + gx)
-                                                : f2{row[wrapx(gx - res_cx(k))], row[wrapx(gx + 1 - res_cx(k))]};
-                    *reinterpret_cast<f2 *>(&L[LJ(k, ly, 2 * px)]) = v;
-                }
-            } else {
-#pragma unroll
-                for (int k = 1; k < Q; ++k)
-                    *reinterpret_cast<f2 *>(&L[LJ(k, ly, 2 * px)]) = *reinterpret_cast<const f2 *>(src + k * P);
-            }
+            for (int k = 1; k < Q; ++k)
+                *reinterpret_cast<f2 *>(&L[LJ(k, ly, 2 * px)]) = *reinterpret_cast<const f2 *>(src + k * P);
             const uint8_t *ob8 = a.obst + (long long)gy * a.nx + gx;
             o0 = ob8[0] != 0;
             o1 = ob8[1] != 0;
@@ -440,14 +408,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             const int gx = ((gx0 + lx) % a.nx + a.nx) % a.nx;
             const int gy = ((gy0 + ly) % a.ny + a.ny) % a.ny;
             const float *src = a.fin + (long long)gy * pitch + gx;
-            if constexpr (AA) {  // read only when a run has zero steps (write-back of pulled state)
 #pragma unroll
-                for (int k = 1; k < Q; ++k)
-                    L[LJ(k, ly, lx)] = a.fin[k * P + (long long)wrapy(gy - res_cy(k)) * pitch + wrapx(gx - res_cx(k))];
-            } else {
-#pragma unroll
-                for (int k = 1; k < Q; ++k) L[LJ(k, ly, lx)] = src[k * P];
-            }
+            for (int k = 1; k < Q; ++k) L[LJ(k, ly, lx)] = src[k * P];
         }
     }
     __syncthreads();
@@ -457,9 +419,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
     };
     const long long deadline_span = a.timeout_ticks;
     int t = 0;
-    // the step body is instantiated per parity (v4's two addressings are
-    // compile-time, so no per-access selects); returns false on abort
-    auto step = [&](auto odd_c) __attribute__((always_inline)) -> bool {
+    // one time step of the tile; returns false on abort
+    auto step = [&]() __attribute__((always_inline)) -> bool {
         const bool tr = a.trace && tile == 0 && threadIdx.x == 0 && t < a.trace_steps;
         if (tr) a.trace[t * 5 + 0] = (long long)wall_clock64();
         if (t > 0 && threadIdx.x == 0) {
@@ -469,7 +430,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             a.partials[(long long)(t - 1) * ntiles + tile] = sw;
         }
         // 1. pull
-        constexpr bool odd = AA && decltype(odd_c)::value;
         f2 s[MAXIT][Q];
 #pragma unroll
         for (int it = 0; it < MAXIT; ++it) {
@@ -480,17 +440,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             }
             const int lx = lxs[it], ly = lys[it];
             s[it][0] = f0[it];
-            if constexpr (AA) {  // all items' loads back to back; no barrier (each slot is this cell's)
-                if (odd) {
-#pragma unroll
-                    for (int k = 1; k < Q; ++k)
-                        s[it][k] = LD2(res_opp(k), ly - res_cy(k), lx - res_cx(k), res_cx(k) == 0);
-                } else {
-#pragma unroll
-                    for (int k = 1; k < Q; ++k) s[it][k] = LD2(k, ly, lx, true);
-                }
-                continue;
-            }
             s[it][1] = f2{L[LJ(1, ly, lx - 1)], L[LJ(1, ly, lx)]};
             s[it][2] = *reinterpret_cast<const f2 *>(&L[LJ(2, ly - 1, lx)]);
             s[it][3] = f2{L[LJ(3, ly, lx + 1)], L[LJ(3, ly, lx + 2)]};
@@ -500,7 +449,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             s[it][7] = f2{L[LJ(7, ly + 1, lx + 1)], L[LJ(7, ly + 1, lx + 2)]};
             s[it][8] = f2{L[LJ(8, ly + 1, lx - 1)], L[LJ(8, ly + 1, lx)]};
         }
-        if constexpr (!AA) __syncthreads();
+        __syncthreads();
         if (tr) a.trace[t * 5 + 1] = (long long)wall_clock64();
         // 2. collide, write back, publish; 3. the neighbours' step-t
         // populations into the ring (the ring slots are read only by the next
@@ -511,20 +460,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         const int slot = t & 1;
         float tot = 0.f;
         bool ok = true;
-        // neighbour's o_k for ring cell (ly, lx): v2 and after an even v4 step
-        // into the ring slot (plane opp k for v4), after an odd v4 step pushed
-        // on into this tile's edge cell (ly, lx) + c_k (dropped when that is
-        // outside the tile: a diagonal tile receives it as a corner granule)
-        auto ring_put = [&](int k, int ly, int lx, float v) {
-            if (!AA) {
-                L[LJ(k, ly, lx)] = v;
-            } else if (!odd) {
-                L[LJ(res_opp(k), ly, lx)] = v;
-            } else {
-                const int ex = lx + res_cx(k), ey = ly + res_cy(k);
-                if (ex >= 0 && ex < tw && ey >= 0 && ey < th) L[LJ(k, ey, ex)] = v;
-            }
-        };
+        // neighbour's o_k for ring cell (ly, lx): into the ring slot
+        auto ring_put = [&](int k, int ly, int lx, float v) { L[LJ(k, ly, lx)] = v; };
         auto poll_ring = [&]() {
             const long long deadline = (long long)wall_clock64() + deadline_span;
             for (int side = wv; side < 4; side += NW) {
@@ -568,16 +505,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
                                   a.omo, a.w1, a.w2);
             tot += u.x + u.y;
             f0[it] = o[0];
-            if (!AA) {
 #pragma unroll
-                for (int k = 1; k < Q; ++k) ST2(k, ly, lx, true, o[k]);
-            } else if (odd) {
-#pragma unroll
-                for (int k = 1; k < Q; ++k) ST2(k, ly + res_cy(k), lx + res_cx(k), res_cx(k) == 0, o[k]);
-            } else {
-#pragma unroll
-                for (int k = 1; k < Q; ++k) ST2(res_opp(k), ly, lx, true, o[k]);
-            }
+            for (int k = 1; k < Q; ++k) ST2(k, ly, lx, true, o[k]);
             const bool west = lx == 0, east = lx + 2 == tw;
             if (ly == th - 1) {  // leaving north: 2, 5, 6
                 unsigned long long *g = gbase(slot, tile, DN) + lx;
@@ -631,8 +560,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         return !abort_flag;
     };
     for (; t < a.steps; ++t) {
-        const bool go = (AA && (t & 1)) ? step(std::true_type{}) : step(std::false_type{});
-        if (!go) break;
+        if (!step()) break;
     }
     if (t == a.steps && a.steps > 0 && threadIdx.x == 0) {
         float sw = wsum[0];
@@ -647,280 +575,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         float *dst = a.fout + (long long)(gy0 + ly) * pitch + gx0 + lx;
         *reinterpret_cast<f2 *>(dst) = f0[it];
 #pragma unroll
-        for (int k = 1; k < Q; ++k) {
-            f2 v;
-            if (!AA)  // v4 after an odd step count: o_k in F[opp k][x]; after an even one: in F[k][x + c_k]
-                v = LD2(k, ly, lx, true);
-            else if (a.steps & 1)
-                v = LD2(res_opp(k), ly, lx, true);
-            else
-                v = LD2(k, ly + res_cy(k), lx + res_cx(k), res_cx(k) == 0);
-            *reinterpret_cast<f2 *>(dst + k * P) = v;
-        }
+        for (int k = 1; k < Q; ++k) *reinterpret_cast<f2 *>(dst + k * P) = LD2(k, ly, lx, true);
     }
 #undef ST2
 #undef LD2
 #undef LJ
-}
-
-// ---------------------------------------------------------------------------
-// v3: register-resident.  Exact 128 x TH tiling (nx % 128 == 0, ny % TH == 0),
-// TH = NW * R: wave w owns tile rows [w R, w R + R) across the full width,
-// lane l owns columns 2l, 2l+1, and the nine population pairs of its R rows
-// stay in REGISTERS for the whole run.  Pull streaming then needs:
-//   x +- 1: a DPP wave shift (left2 / right2, lbm_packed.hpp), lanes 0 / 63
-//           patched from the tile's west / east ring column (LDS);
-//   y +- 1: registers inside a wave; across waves the edge rows each wave
-//           leaves in LDS (its top row's planes 2,5,6, bottom row's 4,7,8);
-//   ring:   granules from the eight neighbour tiles (as v1/v2), polled into
-//           the same LDS slots (south ring = the "top row" of wave -1, north
-//           ring = the "bottom row" of wave NW).
-// Every LDS slot is double-buffered by step parity, so one barrier per step
-// separates writing step t+1's slots from reading step t's.  LDS traffic per
-// cell falls from 16 accesses (v2) to about 3 / R, and the lattice never
-// leaves the register file.
-// ---------------------------------------------------------------------------
-template <int NW, int R>
-__global__ __launch_bounds__(64 * NW) void resident_steps3(ResidentArgs a) {
-    constexpr int TH = NW * R;
-    __shared__ f2 RB[2][NW + 1][3][64];  // [par][w + 1]: planes 2,5,6 of wave w's top row (w = -1: south ring)
-    __shared__ f2 RA[2][NW + 1][3][64];  // [par][w]: planes 4,7,8 of wave w's bottom row (w = NW: north ring)
-    __shared__ float RW[2][3][TH + 2];   // west ring column, planes 1,5,8, rows -1..TH
-    __shared__ float RE[2][3][TH + 2];   // east ring column, planes 3,6,7
-    __shared__ float wsum[NW];
-    __shared__ int abort_flag;
-
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int ntiles = a.tiles_x * a.tiles_y;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-    const int gx0 = tx * RES2_TW, gy0 = ty * TH;
-    const int txe = tx + 1 == a.tiles_x ? 0 : tx + 1, txw = tx == 0 ? a.tiles_x - 1 : tx - 1;
-    const int tyn = ty + 1 == a.tiles_y ? 0 : ty + 1, tys = ty == 0 ? a.tiles_y - 1 : ty - 1;
-    const long long P = a.plane;
-    const int pitch = a.pitch;
-    const int gx = gx0 + 2 * lane;
-    if (threadIdx.x == 0) abort_flag = 0;
-
-    // ---- state into registers, edge rows and ring into LDS (parity 0) -------
-    f2 f[R][Q];
-    unsigned oa = 0, ob = 0, anyo = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int gy = gy0 + wv * R + r;
-        const float *src = a.fin + (long long)gy * pitch + gx;
-#pragma unroll
-        for (int k = 0; k < Q; ++k) f[r][k] = *reinterpret_cast<const f2 *>(src + k * P);
-        const uint8_t *o8 = a.obst + (long long)gy * a.nx + gx;
-        const bool o0 = o8[0] != 0, o1 = o8[1] != 0;
-        oa |= (unsigned)o0 << r;
-        ob |= (unsigned)o1 << r;
-        if (__ballot(o0 || o1) != 0) anyo |= 1u << r;
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        RB[0][wv + 1][i][lane] = f[R - 1][PLANES[DN][i]];
-        RA[0][wv][i][lane] = f[0][PLANES[DS][i]];
-    }
-    auto wrapx = [&](int x) { return (x % a.nx + a.nx) % a.nx; };
-    auto wrapy = [&](int y) { return (y % a.ny + a.ny) % a.ny; };
-    if (wv == 0) {  // south ring row (planes 2,5,6 of global row gy0 - 1)
-        const float *src = a.fin + (long long)wrapy(gy0 - 1) * pitch + gx;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) RB[0][0][i][lane] = *reinterpret_cast<const f2 *>(src + PLANES[DN][i] * P);
-    }
-    if (wv == (NW > 1 ? 1 : 0)) {  // north ring row
-        const float *src = a.fin + (long long)wrapy(gy0 + TH) * pitch + gx;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) RA[0][NW][i][lane] = *reinterpret_cast<const f2 *>(src + PLANES[DS][i] * P);
-    }
-    for (int j = threadIdx.x; j < TH + 2; j += 64 * NW) {  // ring columns, rows -1..TH
-        const long long ry = (long long)wrapy(gy0 + j - 1) * pitch;
-        const float *w = a.fin + ry + wrapx(gx0 - 1), *e = a.fin + ry + wrapx(gx0 + RES2_TW);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            RW[0][i][j] = w[PLANES[DE][i] * P];
-            RE[0][i][j] = e[PLANES[DW][i] * P];
-        }
-    }
-    __syncthreads();
-
-    auto gbase = [&](int slot, int tl, int d) -> unsigned long long * {
-        return a.halo + (((long long)slot * ntiles + tl) * 8 + d) * (3 * RES_GW);
-    };
-    const long long deadline_span = a.timeout_ticks;
-    int t = 0;
-    for (; t < a.steps; ++t) {
-        const int par = t & 1, nxt = par ^ 1;
-        const bool tr = a.trace && tile == 0 && threadIdx.x == 0 && t < a.trace_steps;
-        if (tr) a.trace[t * 5 + 0] = (long long)wall_clock64();
-        if (t > 0 && threadIdx.x == 0) {
-            float sw = wsum[0];
-#pragma unroll
-            for (int i = 1; i < NW; ++i) sw += wsum[i];
-            a.partials[(long long)(t - 1) * ntiles + tile] = sw;
-        }
-        if (tr) a.trace[t * 5 + 1] = (long long)wall_clock64();
-        const unsigned tag = a.tag0 + (unsigned)t + 1u;
-        const int slot = t & 1;
-        float tot = 0.f;
-        float ew[R][6];
-        f2 b2 = RB[par][wv][0][lane], b5 = RB[par][wv][1][lane], b6 = RB[par][wv][2][lane];  // row below
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int y = wv * R + r;  // local row
-            f2 a4, a7, a8;             // row above
-            if (r == R - 1) {
-                a4 = RA[par][wv + 1][0][lane];
-                a7 = RA[par][wv + 1][1][lane];
-                a8 = RA[par][wv + 1][2][lane];
-            } else {
-                a4 = f[r + 1][4];
-                a7 = f[r + 1][7];
-                a8 = f[r + 1][8];
-            }
-            f2 sp[Q];
-            sp[0] = f[r][0];
-            sp[1] = left2(f[r][1]);
-            sp[2] = b2;
-            sp[3] = right2(f[r][3]);
-            sp[4] = a4;
-            sp[5] = left2(b5);
-            sp[6] = right2(b6);
-            sp[7] = right2(a7);
-            sp[8] = left2(a8);
-            const float w1r = RW[par][0][y + 1], w5r = RW[par][1][y], w8r = RW[par][2][y + 2];
-            const float e3r = RE[par][0][y + 1], e6r = RE[par][1][y], e7r = RE[par][2][y + 2];
-            if (lane == 0) {
-                sp[1].x = w1r;
-                sp[5].x = w5r;
-                sp[8].x = w8r;
-            }
-            if (lane == 63) {
-                sp[3].y = e3r;
-                sp[6].y = e6r;
-                sp[7].y = e7r;
-            }
-            // old planes 2,5,6 of this row: the "row below" of row r + 1
-            b2 = f[r][2];
-            b5 = f[r][5];
-            b6 = f[r][6];
-            const float accf = (gy0 + y == a.accel_row) ? 1.00f : 0.00f;
-            const f2 u = collide2(sp, f[r], (oa >> r) & 1u, (ob >> r) & 1u, (anyo >> r) & 1u, accf, a.omega, a.omo,
-                                  a.w1, a.w2);
-            tot += u.x + u.y;
-            const f2 *o = f[r];
-            if (r == R - 1) {
-#pragma unroll
-                for (int i = 0; i < 3; ++i) RB[nxt][wv + 1][i][lane] = o[PLANES[DN][i]];
-                if (wv == NW - 1) {  // leaving north: 2, 5, 6
-                    unsigned long long *g = gbase(slot, tile, DN) + 2 * lane;
-                    publish(g, o[2].x, tag);
-                    publish(g + 1, o[2].y, tag);
-                    publish(g + RES_GW, o[5].x, tag);
-                    publish(g + RES_GW + 1, o[5].y, tag);
-                    publish(g + 2 * RES_GW, o[6].x, tag);
-                    publish(g + 2 * RES_GW + 1, o[6].y, tag);
-                    if (lane == 63) publish(gbase(slot, tile, DNE), o[5].y, tag);
-                    if (lane == 0) publish(gbase(slot, tile, DNW), o[6].x, tag);
-                }
-            }
-            if (r == 0) {
-#pragma unroll
-                for (int i = 0; i < 3; ++i) RA[nxt][wv][i][lane] = o[PLANES[DS][i]];
-                if (wv == 0) {  // leaving south: 4, 7, 8
-                    unsigned long long *g = gbase(slot, tile, DS) + 2 * lane;
-                    publish(g, o[4].x, tag);
-                    publish(g + 1, o[4].y, tag);
-                    publish(g + RES_GW, o[7].x, tag);
-                    publish(g + RES_GW + 1, o[7].y, tag);
-                    publish(g + 2 * RES_GW, o[8].x, tag);
-                    publish(g + 2 * RES_GW + 1, o[8].y, tag);
-                    if (lane == 0) publish(gbase(slot, tile, DSW), o[7].x, tag);
-                    if (lane == 63) publish(gbase(slot, tile, DSE), o[8].y, tag);
-                }
-            }
-            // leaving west: 3, 6, 7 of column 0 (lane 0); east: 1, 5, 8 of column 127 (lane 63)
-            ew[r][0] = rdlane(o[3].x, 0);
-            ew[r][1] = rdlane(o[6].x, 0);
-            ew[r][2] = rdlane(o[7].x, 0);
-            ew[r][3] = rdlane(o[1].y, 63);
-            ew[r][4] = rdlane(o[5].y, 63);
-            ew[r][5] = rdlane(o[8].y, 63);
-        }
-        // the wave's 6R west / east edge granules in ONE store instruction
-        // (single-lane stores are one fabric write each)
-        if (lane < 6 * R) {
-            const int r = lane / 6, q = lane - 6 * r;
-            float v = ew[0][0];
-#pragma unroll
-            for (int rr = 0; rr < R; ++rr)
-#pragma unroll
-                for (int qq = 0; qq < 6; ++qq) v = (lane == 6 * rr + qq) ? ew[rr][qq] : v;
-            publish(gbase(slot, tile, q < 3 ? DW : DE) + (q < 3 ? q : q - 3) * RES_GW + wv * R + r, v, tag);
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) tot += __shfl_down(tot, off, 64);
-        if (lane == 0) wsum[wv] = tot;
-        if (tr) a.trace[t * 5 + 2] = (long long)wall_clock64();
-        // neighbours' step-t outputs -> the ring slots of step t + 1
-        bool ok = true;
-        const long long deadline = (long long)wall_clock64() + deadline_span;
-        for (int side = wv; side < 4; side += NW) {
-            const int len = side < 2 ? RES2_TW : TH;
-            const int src_tile = side == 0 ? tys * a.tiles_x + tx
-                               : side == 1 ? tyn * a.tiles_x + tx
-                               : side == 2 ? ty * a.tiles_x + txw
-                                           : ty * a.tiles_x + txe;
-            const int d = side == 0 ? DN : side == 1 ? DS : side == 2 ? DE : DW;
-            const bool corner = side < 2 && lane < 2, left = lane == 0;
-            const int cd = side == 0 ? (left ? DNE : DNW) : (left ? DSE : DSW);
-            const unsigned long long *cg =
-                corner ? gbase(slot, (side == 0 ? tys : tyn) * a.tiles_x + (left ? txw : txe), cd) : nullptr;
-            float v[7];
-            ok = ok && fetch_ring<2>(gbase(slot, src_tile, d), len, cg, tag, deadline, v);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int p = lane + 64 * j;
-                if (p >= len) continue;
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    if (side == 0) reinterpret_cast<float *>(&RB[nxt][0][i][0])[p] = v[3 * j + i];
-                    else if (side == 1) reinterpret_cast<float *>(&RA[nxt][NW][i][0])[p] = v[3 * j + i];
-                    else if (side == 2) RW[nxt][i][p + 1] = v[3 * j + i];
-                    else RE[nxt][i][p + 1] = v[3 * j + i];
-                }
-            }
-            if (corner) {
-                // below-left NE (5) -> west column row -1; below-right NW (6) -> east column row -1;
-                // above-left SE (8) -> west column row TH; above-right SW (7) -> east column row TH
-                const int row = side == 0 ? 0 : TH + 1;
-                const int i = side == 0 ? 1 : 2;
-                if (left) RW[nxt][i][row] = v[6];
-                else RE[nxt][i][row] = v[6];
-            }
-        }
-        if (tr) a.trace[t * 5 + 3] = (long long)wall_clock64();
-        if (!ok) {
-            abort_flag = 1;
-            __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (tr) a.trace[t * 5 + 4] = (long long)wall_clock64();
-        if (abort_flag) break;
-    }
-    if (t == a.steps && a.steps > 0 && threadIdx.x == 0) {
-        float sw = wsum[0];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) sw += wsum[i];
-        a.partials[(long long)(a.steps - 1) * ntiles + tile] = sw;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        float *dst = a.fout + (long long)(gy0 + wv * R + r) * pitch + gx;
-#pragma unroll
-        for (int k = 0; k < Q; ++k) *reinterpret_cast<f2 *>(dst + k * P) = f[r][k];
-    }
 }
 
 // av_local[t] = sum over tiles of partials[t][tile], fixed order (one wave per step).
@@ -943,15 +602,11 @@ const void *resident_fn() {
     return reinterpret_cast<const void *>(&resident_steps<NW, R>);
 }
 
-template <int NW, int TH, int MINW = 1, bool AA = false>
+template <int NW, int TH, int MINW = 1>
 const void *resident_fn2() {
-    return reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW, AA>);
+    return reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW>);
 }
 
-template <int NW, int R>
-const void *resident_fn3() {
-    return reinterpret_cast<const void *>(&resident_steps3<NW, R>);
-}
 
 const void *resident_kernel(int variant, int &threads) {
     switch (variant) {
@@ -966,19 +621,7 @@ const void *resident_kernel(int variant, int &threads) {
         case RES2_16x8: threads = 512; return resident_fn2<8, 16, 4>();  // 2 blocks per CU: 4 waves per SIMD
         case RES2_8: threads = 512; return resident_fn2<8, 8>();
         case RES2_4: threads = 256; return resident_fn2<4, 4>();
-        case RES2_2: threads = 128; return resident_fn2<2, 2>();
-        case RES4_32: threads = 1024; return resident_fn2<16, 32, 1, true>();
-        case RES4_16: threads = 1024; return resident_fn2<16, 16, 1, true>();
-        case RES4_8: threads = 512; return resident_fn2<8, 8, 1, true>();
-        case RES4_4: threads = 256; return resident_fn2<4, 4, 1, true>();
-        case RES4_2: threads = 128; return resident_fn2<2, 2, 1, true>();
-        case RES4_16x8: threads = 512; return resident_fn2<8, 16, 4, true>();
-        case RES3_32: threads = 1024; return resident_fn3<16, 2>();
-        case RES3_32x8: threads = 512; return resident_fn3<8, 4>();
-        case RES3_16: threads = 512; return resident_fn3<8, 2>();
-        case RES3_8: threads = 256; return resident_fn3<4, 2>();
-        case RES3_4: threads = 256; return resident_fn3<4, 1>();
-        default: threads = 128; return resident_fn3<2, 1>();  // RES3_2
+        default: threads = 128; return resident_fn2<2, 2>();  // RES2_2
     }
 }
 }  // namespace

@@ -294,16 +294,9 @@ static void launch_w(const Step2Args &a, int blocks, bool reduce, hipStream_t s)
 // Tile shapes offered (Tile2 in lbm_layout.hpp); the engine picks one at create.
 hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t s) {
     switch (a.tile) {
-        case T2V_64x16_W8: launch_w<16, 8>(a, blocks, reduce, s); break;
         case T2V_64x8_W8: launch_w<8, 8>(a, blocks, reduce, s); break;
-        case T2V_64x16_W4: launch_w<16, 4>(a, blocks, reduce, s); break;
-        case T2V_64x8_W4: launch_w<8, 4>(a, blocks, reduce, s); break;
-        case T2V_64x32_W8: launch_w<32, 8>(a, blocks, reduce, s); break;
         case T2_64x8: launch_tile<64, 8>(a, blocks, reduce, s); break;
-        case T2_128x8: launch_tile<128, 8>(a, blocks, reduce, s); break;
-        case T2_32x16: launch_tile<32, 16>(a, blocks, reduce, s); break;
-        case T2_64x24: launch_tile<64, 24>(a, blocks, reduce, s); break;
-        default: launch_tile<64, 16>(a, blocks, reduce, s); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

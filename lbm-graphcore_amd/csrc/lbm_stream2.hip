@@ -1,180 +1,28 @@
-// lbm_stream2.hip -- S-step register-streaming kernel, two columns per lane,
-// packed fp32 arithmetic.
+// lbm_stream2.hip -- the S-step register-streaming kernel (stream_steps2d),
+// two columns per lane, packed fp32 arithmetic: the default fused kernel
+// for sub-domains of 4 M cells and more.
 //
-// Same schedule as lbm_stream.hip (one wave walks a strip row by row, level L
-// computes row j-L of step t+L as input row j arrives; lattice through HBM
-// once per S steps), but each lane owns TWO adjacent columns (xa = base + 2l,
-// xb = xa + 1):
+// One wave walks a strip of 128 columns row by row; as input row j arrives,
+// level L computes row j-L of time step t+L, so the lattice crosses HBM once
+// per S steps.  Each lane owns TWO adjacent columns (xa = base + 2l, xb = xa + 1):
 //   * loads and stores are float2 (512 B per wave and plane row);
 //   * the x-1 / x+1 neighbours are half in-lane (B's left is A, A's right is
 //     B) and half one DPP wave shift away, so a shift costs one v_mov_dpp per
 //     two cells;
 //   * the two cells' arithmetic runs as packed fp32 (v_pk_add_f32 /
-//     v_pk_mul_f32 / v_pk_fma_f32 on ext_vector_type(2) float), halving the
-//     VALU instructions of the collision, which bounds the fused kernels;
+//     v_pk_mul_f32 / v_pk_fma_f32 on ext_vector_type(2) float);
 //   * a 128-column strip recomputes 2S (+2 when its first column has the
-//     wrong parity for float2 alignment) of every 128 columns instead of 2S
-//     of 64.
+//     wrong parity for float2 alignment) of every 128 columns.
 //
 // Bitwise parity with the one-step kernels and the CPU oracle: the packed
 // collision and its exact short division / sqrt sequences live in
-// lbm_packed.hpp (shared with the packed resident kernel).
-// The GPU parity tests (bitwise lattice vs the oracle on every reference
-// grid and on randomized problems) check all of it end to end.
+// lbm_packed.hpp (shared with the packed resident kernel); the
+// LBM_FLAG_TOLERANCE form (collide2t) is checked against a stated tolerance
+// instead (tests/test_gpu_tolerance.py).
 
 #include "lbm_packed.hpp"
 
 namespace lbm {
-
-__device__ __forceinline__ float stream2_accel(const StreamArgs &a, int y) {
-    int g = a.gy0 + y;
-    g = g < 0 ? g + a.ny : (g >= a.ny ? g - a.ny : g);
-    return (g == a.accel_g) ? 1.00f : 0.00f;
-}
-
-__device__ __forceinline__ void halo_out(const StreamArgs &a, int S, int x, int y, const float (&o)[Q]) {
-    const bool east = x >= a.w - S, west = x < S, north = y >= a.h - S, south = y < S;
-    if (east) store2(a.dst[DE], x - (a.w - S), y, o);
-    if (west) store2(a.dst[DW], x, y, o);
-    if (north) {
-        store2(a.dst[DN], y - (a.h - S), x, o);
-        if (east) store2(a.dst[DNE], y - (a.h - S), x - (a.w - S), o);
-        if (west) store2(a.dst[DNW], y - (a.h - S), x, o);
-    }
-    if (south) {
-        store2(a.dst[DS], y, x, o);
-        if (west) store2(a.dst[DSW], y, x, o);
-        if (east) store2(a.dst[DSE], y, x - (a.w - S), o);
-    }
-}
-
-template <int S, bool kReduce, int MINW>
-__global__ __launch_bounds__(64, MINW) void stream_steps2c(StreamArgs a) {
-    __shared__ float lds[1];
-    if (kReduce && blockIdx.x == 0) reduce_pending_n<64>(a.ctl, a.partials_prev, a.av_local, lds);
-
-    const int lane = threadIdx.x;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
-    f2 tot[S];
-#pragma unroll
-    for (int l = 0; l < S; ++l) tot[l] = mk2(0.f);
-
-    if (t < a.total) {
-        const int r = rect_of(a.rect_begin, t);
-        const SRect R = a.rect[r];
-        const int lt = t - a.rect_begin[r];
-        const int seg = lt / R.nstrip, strip = lt - seg * R.nstrip;
-        const int xo0 = R.x0 + strip * R.ow;             // first owned column
-        const int xo1 = min(xo0 + R.ow, R.x0 + R.w);     // past the last owned column
-        const int base = (xo0 - S) & ~1;                 // even: float2-aligned
-        const int xa = base + 2 * lane, xb = xa + 1;
-        const bool owna = xa >= xo0 && xa < xo1, ownb = xb >= xo0 && xb < xo1;
-        const int yo0 = R.y0 + seg * R.hs;
-        const int yo1 = min(yo0 + R.hs, R.y0 + R.h);
-        const int xca = min(xa, (a.xmax - 1) & ~1);
-        const long long P = a.plane;
-        const int pitch = a.pitch;
-        const float *src = a.fin + xca;
-        const uint8_t *obp = a.obst_g + (xca + a.og);
-        const int jlast = yo1 + S - 1;
-
-        f2 c0[S], c1[S], c3[S], a2[S], a5[S], a6[S], b2[S], b5[S], b6[S];
-#pragma unroll
-        for (int b = 0; b < S; ++b)
-            c0[b] = c1[b] = c3[b] = a2[b] = a5[b] = a6[b] = b2[b] = b5[b] = b6[b] = mk2(0.f);
-        unsigned oba = 0, obb = 0;
-
-        int j = yo0 - S;
-        f2 v[Q];
-        unsigned voa, vob;
-        {
-            const float *c = src + (long long)j * pitch;
-#pragma unroll
-            for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const f2 *>(c + k * P);
-            const uint8_t *oc = obp + (long long)(j + a.og) * a.ogp;
-            voa = oc[0];
-            vob = oc[1];
-        }
-        for (; j <= jlast; ++j) {
-            const int jn = min(j + 1, jlast);
-            f2 nv[Q];
-            const float *cn = src + (long long)jn * pitch;
-#pragma unroll
-            for (int k = 0; k < Q; ++k) nv[k] = *reinterpret_cast<const f2 *>(cn + k * P);
-            const uint8_t *ocn = obp + (long long)(jn + a.og) * a.ogp;
-            const unsigned nvoa = ocn[0], nvob = ocn[1];
-
-            oba = (oba << 1) | (voa != 0 ? 1u : 0u);
-            obb = (obb << 1) | (vob != 0 ? 1u : 0u);
-            f2 cur[Q];
-#pragma unroll
-            for (int k = 0; k < Q; ++k) cur[k] = v[k];
-#pragma unroll
-            for (int L = 1; L <= S; ++L) {
-                const int b = L - 1;
-                const int y = j - L;
-                const f2 s[Q] = {c0[b], c1[b], b2[b], c3[b], cur[4], b5[b], b6[b], right2(cur[7]), left2(cur[8])};
-                b2[b] = a2[b];
-                b5[b] = a5[b];
-                b6[b] = a6[b];
-                a2[b] = cur[2];
-                a5[b] = left2(cur[5]);
-                a6[b] = right2(cur[6]);
-                c0[b] = cur[0];
-                c1[b] = left2(cur[1]);
-                c3[b] = right2(cur[3]);
-
-                f2 o[Q];
-                const bool oa = (oba >> L) & 1u, ob = (obb >> L) & 1u;
-                const bool any_obst = __builtin_amdgcn_ballot_w64(oa || ob) != 0;
-                const f2 u = collide2(s, o, oa, ob, any_obst, stream2_accel(a, y), a.omega, a.omo, a.w1, a.w2);
-                const bool rowlive = y >= yo0 && y < yo1;
-                if (rowlive) tot[b] += f2{owna ? u.x : 0.f, ownb ? u.y : 0.f};
-                if (L == S) {
-                    if (rowlive && (owna || ownb)) {
-                        float *w0 = a.fout + (long long)y * pitch + xa;
-                        if (owna && ownb) {
-#pragma unroll
-                            for (int k = 0; k < Q; ++k) *reinterpret_cast<f2 *>(w0 + k * P) = o[k];
-                        } else if (owna) {
-#pragma unroll
-                            for (int k = 0; k < Q; ++k) w0[k * P] = o[k].x;
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < Q; ++k) w0[k * P + 1] = o[k].y;
-                        }
-                        if (xa < S || xb >= a.w - S || y < S || y >= a.h - S) {
-                            float oa_[Q], ob_[Q];
-#pragma unroll
-                            for (int k = 0; k < Q; ++k) {
-                                oa_[k] = o[k].x;
-                                ob_[k] = o[k].y;
-                            }
-                            if (owna) halo_out(a, S, xa, y, oa_);
-                            if (ownb) halo_out(a, S, xb, y, ob_);
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < Q; ++k) cur[k] = o[k];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < Q; ++k) v[k] = nv[k];
-            voa = nvoa;
-            vob = nvob;
-        }
-    }
-
-#pragma unroll
-    for (int l = 0; l < S; ++l) {
-        float sum = tot[l].x + tot[l].y;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
-        if (lane == 0) a.partials_out[(long long)l * a.stride + blockIdx.x] = sum;
-    }
-    if (kReduce && blockIdx.x == 0 && lane == 0) publish_pending(a.ctl, S, a.n_total, a.stride);
-}
 
 // halo_out with the destinations read from device memory inside the (rare)
 // branch that stores them, so they hold no scalar registers across the loop
@@ -231,9 +79,9 @@ __device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, in
 }
 
 // ---------------------------------------------------------------------------
-// stream_steps2d: the same schedule and arithmetic as stream_steps2c with the
-// work the streaming order makes redundant removed (every lattice value and
-// every |u| partial bitwise unchanged):
+// stream_steps2d: the work the streaming order makes redundant is removed
+// (round 2 against its predecessor, every lattice value and every |u| partial
+// bitwise unchanged):
 //   * level L's first 2L row iterations of a segment would compute rows whose
 //     own inputs were never loaded (their results are never used): they are
 //     skipped (a warm-up loop of 2S iterations with wave-uniform guards, then
@@ -644,37 +492,6 @@ hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduc
         case 43: launch_s2d<4, true>(a, units, reduce, s); break;
         case 53: launch_s2d<5, true>(a, units, reduce, s); break;
         case 63: launch_s2d<6, true>(a, units, reduce, s); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template <int S, int MINW>
-static void launch_s2c(const StreamArgs &a, int blocks, bool reduce, hipStream_t s) {
-    if (reduce)
-        hipLaunchKernelGGL((stream_steps2c<S, true, MINW>), dim3(blocks), dim3(64), 0, s, a);
-    else
-        hipLaunchKernelGGL((stream_steps2c<S, false, MINW>), dim3(blocks), dim3(64), 0, s, a);
-}
-
-// Resident 64-thread blocks (waves) per CU of the instantiation a launch with
-// these parameters uses (the engine sizes segments to whole rounds of them).
-hipError_t stream2c_blocks_per_cu(int steps, int waves, int &n) {
-    const bool w3 = waves >= 3;
-    const void *fn = steps == 2   ? (const void *)&stream_steps2c<2, false, 2>
-                     : steps == 3 ? (w3 ? (const void *)&stream_steps2c<3, false, 3> : (const void *)&stream_steps2c<3, false, 2>)
-                                  : (w3 ? (const void *)&stream_steps2c<4, false, 3> : (const void *)&stream_steps2c<4, false, 2>);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, 0);
-}
-
-// waves = minimum waves per SIMD the register allocation targets (2, or 3:
-// fewer registers, some spilled)
-hipError_t launch_stream2c(const StreamArgs &a, int blocks, int steps, bool reduce, int waves, hipStream_t s) {
-    const bool w3 = waves >= 3;
-    switch (steps) {
-        case 2: launch_s2c<2, 2>(a, blocks, reduce, s); break;
-        case 3: w3 ? launch_s2c<3, 3>(a, blocks, reduce, s) : launch_s2c<3, 2>(a, blocks, reduce, s); break;
-        case 4: w3 ? launch_s2c<4, 3>(a, blocks, reduce, s) : launch_s2c<4, 2>(a, blocks, reduce, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -25,7 +25,7 @@ for p in (str(ROOT), str(PKG)):
 
 from lbm_amd import io as lio  # noqa: E402
 
-# The library reads its tuning knobs (LBM_STREAM_V, LBM_TILE2, ...) only with
+# The library reads its tuning knobs (LBM_STREAM_CFG, LBM_TILE2, ...) only with
 # LBM_DEBUG_KNOBS=1; the tests that select variants through them need it.
 # Unset knobs keep the product defaults.
 os.environ.setdefault("LBM_DEBUG_KNOBS", "1")

@@ -288,10 +288,11 @@ def test_forced_exchange_bitwise(gpu_lib, transport, parts, grid, mode):
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
-@pytest.mark.parametrize("tile", list(range(10)))
+@pytest.mark.parametrize("tile", [0, 1])
 def test_step2_tile_variants_bitwise(gpu_lib, tile, monkeypatch):
-    """Every fused two-step tile shape (v1 LDS-only and v2 wave-per-row) is
-    bitwise identical to the oracle: whole domain, 4-way loop-back, ragged."""
+    """Both fused two-step tile shapes (v1 LDS-only 64x8 and v2 wave-per-row
+    64x8) are bitwise identical to the oracle: whole domain, 4-way loop-back,
+    ragged."""
     monkeypatch.setenv("LBM_TILE2", str(tile))
     p, obst = load_problem("128x256", iters=11)
     cells0 = lio.init_cells(p)
@@ -313,19 +314,18 @@ def test_step2_tile_variants_bitwise(gpu_lib, tile, monkeypatch):
     np.testing.assert_allclose(av, r2av, rtol=1e-5)
 
 
-@pytest.mark.parametrize("version", [1, 2, 3])
-@pytest.mark.parametrize("S", [2, 3, 4])
+@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (5, 4), (7, 4), (8, 4)])
 @pytest.mark.parametrize("hs", [1, 7, 100000])
-def test_stream_segments_bitwise(gpu_lib, version, S, hs, monkeypatch):
-    """Stream kernels (one / two columns per lane) with segment heights from
+def test_stream_segments_bitwise(gpu_lib, S, cfg, hs, monkeypatch):
+    """The stream kernel (plain and LP launch forms) with segment heights from
     one row to the whole sub-domain (re-streamed overlap rows at every segment
     seam), single domain and 2x2 loop-back, step counts with and without a
     one-step remainder."""
     monkeypatch.setenv("LBM_STREAM_HS", str(hs))
-    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    monkeypatch.setenv("LBM_STREAM_CFG", str(cfg))
     p, obst = load_problem("128x256", iters=13)
     cells0 = lio.init_cells(p)
-    for steps in (12, 13):
+    for steps in (2 * S + 2, 2 * S + 3):
         ref, ref_av = oracle.run(p, obst, steps, cells0)
         for kw in (dict(), dict(parts=4, grid=(2, 2), devices=[0])):
             cells, av, used = gpu_run(gpu_lib, p, obst, cells0, steps, kernel=gpu_lib.KERNEL_STREAM,
@@ -397,17 +397,14 @@ def test_stream_size_limits(gpu_lib):
         assert e.kernel_in_use() in ("step2", "stream")
 
 
-@pytest.mark.parametrize("version", [1, 2, 3])
-@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5"])
-def test_open_periodic_random_bitwise(gpu_lib, mode, version, monkeypatch):
+@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5", "stream6", "lp7", "lp8"])
+def test_open_periodic_random_bitwise(gpu_lib, mode, monkeypatch):
     """No walls: flow crosses every periodic seam and every sub-domain seam.
     Random sparse obstacles, perturbed populations, odd sizes; single domain
     and 2x2 / 3x2 loop-back decompositions."""
-    if mode == "step2" and version != 1:
-        pytest.skip("one step2 variant")
-    if mode == "stream5" and version != 3:
-        pytest.skip("5 steps per launch: v3 kernel only")
-    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    if mode.startswith("lp"):  # LP launch form (LBM_STREAM_CFG=4)
+        monkeypatch.setenv("LBM_STREAM_CFG", "4")
+        mode = "stream" + mode[2:]
     rng = np.random.default_rng(7)
     p = lio.Params(150, 70, 9, 10, 0.1, 0.02, 1.7)
     obst = (rng.random((70, 150)) < 0.05).astype(np.uint8)
@@ -423,9 +420,7 @@ def test_open_periodic_random_bitwise(gpu_lib, mode, version, monkeypatch):
 # ------------------------------------------------- resident kernel ----
 
 # (version, tile height): v1 scalar 64-column tiles, v2 packed 128-column tiles
-# v3 register-resident, exact 128 x TH tilings only; v4 = v2 tiles, AA-pattern LDS
-RES_VARIANTS = [(1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 2), (2, 4), (2, 8), (2, 16), (2, 32),
-                (3, 2), (3, 4), (3, 8), (3, 16), (3, 32), (4, 2), (4, 4), (4, 8), (4, 16), (4, 32)]
+RES_VARIANTS = [(1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 2), (2, 4), (2, 8), (2, 16), (2, 32)]
 
 
 @pytest.mark.parametrize("ver,th", RES_VARIANTS)
@@ -434,10 +429,8 @@ RES_VARIANTS = [(1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 2), (2, 4), (2, 8
 def test_resident_tiles_bitwise(gpu_lib, ver, th, nx, ny, steps, monkeypatch):
     """Every resident tile height on exact and ragged tilings (partial last tiles in
     x and y, one-row and one-column grids): lattice bitwise == oracle."""
-    if ver in (2, 4) and nx % 2:
+    if ver == 2 and nx % 2:
         pytest.skip("the packed resident kernel needs an even width")
-    if ver == 3 and (nx % 128 or ny % th):
-        pytest.skip("the register-resident kernel needs an exact 128 x TH tiling")
     monkeypatch.setenv("LBM_RES_TH", str(th))
     monkeypatch.setenv("LBM_RES_V", str(ver))
     p = lio.Params(nx, ny, steps, 10, 0.1, 0.02, 1.7)
@@ -455,7 +448,7 @@ def test_resident_tiles_bitwise(gpu_lib, ver, th, nx, ny, steps, monkeypatch):
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
-@pytest.mark.parametrize("ver", [1, 2, 3, 4])
+@pytest.mark.parametrize("ver", [1, 2])
 def test_resident_1024_runs_continue(gpu_lib, ver, monkeypatch):
     """1024^2 (BASELINE config 2 grid, 256 co-resident 64x64 tiles): three runs of
     different lengths continue one state (granule tags keep counting across runs),
@@ -544,19 +537,18 @@ def test_pipeline_reference_grid_full_run(gpu_lib, grid, tmp_path):
 # ------------------------------------- wide decomposed x bands (stream) ----
 
 @pytest.mark.parametrize("nx", [1030, 1031])
-@pytest.mark.parametrize("version", [1, 2, 3])
-@pytest.mark.parametrize("S", [2, 3, 4])
-def test_stream_wide_x_bands_bitwise(gpu_lib, nx, version, S, monkeypatch):
+@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 4), (8, 4)])
+def test_stream_wide_x_bands_bitwise(gpu_lib, nx, S, cfg, monkeypatch):
     """Sub-domains wide enough (>= 4 strips) for the strip-wide x boundary band
     of a decomposed x side (lbm_engine.hip stream_split: xb = one strip, the
     right band's owned width depending on its first column's parity, the
     interior starting at x0 = xb): 1x2 and 2x2 loop-back with widths 515/516,
     an odd total width, a one-step remainder, and the forced-exchange variant
     (every wrap through the transport) -- bitwise vs the oracle."""
-    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    monkeypatch.setenv("LBM_STREAM_CFG", str(cfg))
     ny = 40
     p = lio.Params(nx, ny, 9, 10, 0.1, 0.02, 1.7)
-    rng = np.random.default_rng(nx + 10 * S + version)
+    rng = np.random.default_rng(nx + 10 * S + cfg)
     obst = (rng.random((ny, nx)) < 0.03).astype(np.uint8)
     obst[:, 500:503] = 1  # a wall across the band seam region
     cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((ny, nx, 9)))).astype(np.float32)
@@ -589,20 +581,17 @@ def _adversarial_state(nx, ny, seed):
     return cells.astype(np.float32)
 
 
-@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "resident", "vec4", "step2"])
-@pytest.mark.parametrize("version", [2, 3])
-def test_division_adversarial_states_bitwise(gpu_lib, mode, version, monkeypatch):
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp8", "resident", "vec4", "step2"])
+def test_division_adversarial_states_bitwise(gpu_lib, mode, monkeypatch):
     """lbm_packed.hpp's short division sequences (x/9, x/36 by multiply + two
     corrections; n/rho without v_div_scale / v_div_fixup) against the oracle's
     correctly rounded '/' on states where the momentum numerators are zero,
     tiny normal or subnormal and rho spans many binades (down to the smallest
     normals): the lattice must stay bitwise equal.  One step and three steps,
     no obstacles and no acceleration (so the states stay in their binades)."""
-    if version == 3 and not mode.startswith("stream"):
-        pytest.skip("LBM_STREAM_V only selects the stream kernel")
-    if mode == "stream5" and version != 3:
-        pytest.skip("5 steps per launch: v3 kernel only")
-    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    if mode.startswith("lp"):
+        monkeypatch.setenv("LBM_STREAM_CFG", "4")
+        mode = "stream" + mode[2:]
     monkeypatch.setenv("LBM_RES_V", "2")  # the packed resident kernel (collide2)
     nx, ny = 256, 66
     p = lio.Params(nx, ny, 3, 10, 0.1, 0.0, 1.85)
@@ -616,13 +605,12 @@ def test_division_adversarial_states_bitwise(gpu_lib, mode, version, monkeypatch
         if not same.all():
             bad = np.argwhere(~same)
             y, x, k = bad[0]
-            pytest.fail(f"{mode} v{version} {steps} steps: {len(bad)} values differ, first at y={y} x={x} k={k}: "
+            pytest.fail(f"{mode} {steps} steps: {len(bad)} values differ, first at y={y} x={x} k={k}: "
                         f"gpu {cells[y, x, k]!r} oracle {ref[y, x, k]!r}")
 
 
-@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "resident", "vec4", "step2"])
-@pytest.mark.parametrize("version", [2, 3])
-def test_signed_zero_states_bitwise(gpu_lib, mode, version, monkeypatch):
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp8", "resident", "vec4", "step2"])
+def test_signed_zero_states_bitwise(gpu_lib, mode, monkeypatch):
     """The folded acceleration is added on EVERY row as accel * w
     (LastChance.cpp:253-261: + 0 * w1 off the accelerated row), which turns a
     -0.0 post-collision population into +0.0.  A state whose density
@@ -630,11 +618,9 @@ def test_signed_zero_states_bitwise(gpu_lib, mode, version, monkeypatch):
     produces -0.0 populations on every row; a kernel that skipped the add off
     the accelerated row would keep them negative.  Bitwise vs the oracle,
     NaN positions equal (their payloads are not compared)."""
-    if version == 3 and not mode.startswith("stream"):
-        pytest.skip("LBM_STREAM_V only selects the stream kernel")
-    if mode == "stream5" and version != 3:
-        pytest.skip("5 steps per launch: v3 kernel only")
-    monkeypatch.setenv("LBM_STREAM_V", str(version))
+    if mode.startswith("lp"):
+        monkeypatch.setenv("LBM_STREAM_CFG", "4")
+        mode = "stream" + mode[2:]
     monkeypatch.setenv("LBM_RES_V", "2")
     nx, ny = 256, 66
     p = lio.Params(nx, ny, 3, 10, 0.1, 0.005, 1.85)
@@ -649,12 +635,12 @@ def test_signed_zero_states_bitwise(gpu_lib, mode, version, monkeypatch):
         cells, _, used = gpu_run(gpu_lib, p, obst, cells0, steps, **mode_kw(gpu_lib, mode))
         assert used == kname(mode)
         nan_g, nan_r = np.isnan(cells), np.isnan(ref)
-        assert np.array_equal(nan_g, nan_r), f"{mode} v{version} {steps} steps: NaN positions differ"
+        assert np.array_equal(nan_g, nan_r), f"{mode} {steps} steps: NaN positions differ"
         same = (cells.view(np.uint32) == ref.view(np.uint32)) | nan_r
         if not same.all():
             bad = np.argwhere(~same)
             y, x, k = bad[0]
-            pytest.fail(f"{mode} v{version} {steps} steps: {len(bad)} values differ, first at y={y} x={x} k={k}: "
+            pytest.fail(f"{mode} {steps} steps: {len(bad)} values differ, first at y={y} x={x} k={k}: "
                         f"gpu {cells[y, x, k]!r} oracle {ref[y, x, k]!r}")
 
 
@@ -681,15 +667,12 @@ def test_local_load_store_matches_full(gpu_lib, parts, grid):
     assert np.array_equal(av, av_full)
 
 
-@pytest.mark.parametrize("S", [4, 5, 6])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("S,cfg", [(4, 0), (5, 0), (6, 0), (4, 3), (5, 3), (6, 3), (5, 4), (6, 4), (7, 4), (8, 4)])
 def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, S, monkeypatch):
-    """The v3 stream kernel's launch forms (LBM_STREAM_CFG: one wave per
-    workgroup; four waves taking adjacent strips; four waves with non-temporal
-    lattice stores; one wave with non-temporal stores), 4 to 6 steps per launch, and its guided segment tiers:
-    bitwise vs the oracle on a single domain, 2x2 and 1x3 loop-back, and with
-    one-step remainders."""
-    monkeypatch.setenv("LBM_STREAM_V", "3")
+    """The stream kernel's launch forms (LBM_STREAM_CFG: 0 plain stores, 3
+    non-temporal lattice stores, 4 LP: older plane rows in LDS, up to 8 steps
+    per launch) and its guided segment tiers: bitwise vs the oracle on a
+    single domain, 2x2 and 1x3 loop-back, and with one-step remainders."""
     monkeypatch.setenv("LBM_STREAM_CFG", str(cfg))
     monkeypatch.setenv("LBM_STREAM_GUIDE", "24:0.6,8:0.3,3")
     rng = np.random.default_rng(cfg)

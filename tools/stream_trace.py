@@ -7,7 +7,7 @@ interior launch, then prints: launch span, wave-duration spread, the share of
 the device's wave slots kept busy (sum of wave durations / (slots x span)),
 the busy-slot profile over time, and per-XCD first start / last end.
 
-  LBM_STREAM_V=3 python tools/stream_trace.py --n 8192 --slots 2048
+  LBM_DEBUG_KNOBS=1 python tools/stream_trace.py --n 8192 --slots 2048
 """
 from __future__ import annotations
 
