@@ -569,8 +569,7 @@ def main() -> int:
                                    f"exchange overlapped with the interior" if n > 1 else "single GPU"),
                    "kernel": kernel_used},
         "settle": m["settle"],
-        "roofline": {"bound": "valu" if kernel_used == "stream" else "hbm",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": BYTES_PER_UPDATE * cells_per_gpu,
                      "cell_updates_per_launch": steps_per_launch * cells_per_gpu,

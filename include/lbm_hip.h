@@ -257,6 +257,12 @@ int lbm_placement_probe(lbm_handle *h, int32_t *kept, int32_t *tried, float *ms_
  * fused launches run the LBM_FLAG_TOLERANCE collision. */
 int32_t lbm_numerics(lbm_handle *h);
 
+/* Debug scan: number of NaN / +-Inf populations in the current
+ * lattice of this handle's sub-domains.  With LBM_NAN_CHECK=1 in the
+ * environment every lbm_run / lbm_run_steps ends with this scan and fails
+ * with LBM_E_INTERNAL when it finds any. */
+int lbm_nonfinite_count(lbm_handle *h, int64_t *count);
+
 /* Hash of the library's sources (csrc/, include/) at build time; the Python
  * binding refuses a library whose hash differs from the sources beside it. */
 const char *lbm_source_hash(void);

@@ -53,6 +53,8 @@ hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pit
 hipError_t launch_init_equilibrium(float *base, long long rows, int rf, int pitch, long long P, float c0, float c1,
                                    float c2, hipStream_t s);
 hipError_t launch_aos_to_soa(const float *aos, float *f, long long P, int pitch, int w, int h, hipStream_t s);
+hipError_t launch_count_nonfinite(const float *f, long long P, int pitch, int w, int h, unsigned long long *out,
+                                  hipStream_t s);
 hipError_t launch_soa_to_aos(const float *f, float *aos, long long P, int pitch, int w, int h, hipStream_t s);
 hipError_t launch_halo_pack(const HaloArgs &a, hipStream_t s);
 hipError_t launch_halo_unpack(const HaloArgs &a, hipStream_t s);
@@ -224,6 +226,7 @@ struct lbm_handle {
     int probe_kept = -1;          // the pair kept (-1: no probe)
     bool debug_knobs = false;     // LBM_DEBUG_KNOBS=1: the tuning knobs below are read from the environment
     bool poison = false;          // LBM_POISON=1: fresh allocations filled with NaN bytes (read-before-write check)
+    bool nan_check = false;       // LBM_NAN_CHECK=1: every run ends with a scan of the lattice for NaN / Inf
     bool tolerance = false;       // LBM_FLAG_TOLERANCE: stream kernel with the reciprocal collision (not bitwise)
     int run_fused = 0, run_single = 0;  // launches of the last run: fused (spl steps) / one-step
     // Tuning knobs (environment, read at create): LBM_TWO_STEP, LBM_MAX_BLOCKS,
@@ -280,6 +283,7 @@ struct lbm_handle {
     void read_tuning() {
         debug_knobs = env_int("LBM_DEBUG_KNOBS", 0) != 0;
         poison = env_int("LBM_POISON", 0) != 0;
+        nan_check = env_int("LBM_NAN_CHECK", 0) != 0;
         max_blocks_cfg = std::max(1, knob("LBM_MAX_BLOCKS", max_blocks_cfg));
         graph_steps = std::max(0, knob("LBM_GRAPH_STEPS", graph_steps));
         fused = knob("LBM_TWO_STEP", fused ? 1 : 0) != 0;
@@ -1707,6 +1711,35 @@ struct lbm_handle {
         }
     }
 
+    // NaN / Inf populations in the current lattices of every local sub-domain
+    long long nonfinite_count() {
+        if (!loaded) throw lbm_failure(LBM_E_STATE, "nothing to scan");
+        sync_all();
+        long long total = 0;
+        for (auto &s : subs) {
+            set_device(s);
+            unsigned long long *d = nullptr, hcount = 0;
+            HIP_CHECK(hipMalloc(&d, sizeof(unsigned long long)));
+            HIP_CHECK(hipMemsetAsync(d, 0, sizeof(unsigned long long), s.s_comp));
+            const hipError_t e = launch_count_nonfinite(s.o[s.cur], s.plane, s.pitch, s.w, s.h, d, s.s_comp);
+            if (e == hipSuccess) (void)hipMemcpyAsync(&hcount, d, sizeof(hcount), hipMemcpyDeviceToHost, s.s_comp);
+            const hipError_t e2 = hipStreamSynchronize(s.s_comp);
+            (void)hipFree(d);
+            HIP_CHECK(e);
+            HIP_CHECK(e2);
+            total += (long long)hcount;
+        }
+        return total;
+    }
+
+    void check_finite_after_run() {
+        if (!nan_check) return;
+        const long long bad = nonfinite_count();
+        if (bad > 0)
+            throw lbm_failure(LBM_E_INTERNAL, "LBM_NAN_CHECK: " + std::to_string(bad) +
+                                                  " non-finite populations in the lattice after the run");
+    }
+
     void init_equilibrium() {
         const float c0 = p.density * 4.f / 9.f, c1 = p.density / 9.f, c2 = p.density / 36.f;
         for (auto &s : subs) {
@@ -1947,12 +1980,23 @@ int lbm_init_equilibrium(lbm_handle *h) {
 
 int lbm_run(lbm_handle *h) {
     if (!h) return LBM_E_INVALID;
-    return guarded(h, [&] { h->run_steps(h->p.max_iters, true); });
+    return guarded(h, [&] {
+        h->run_steps(h->p.max_iters, true);
+        h->check_finite_after_run();
+    });
 }
 
 int lbm_run_steps(lbm_handle *h, int32_t steps, int32_t accelerate_first) {
     if (!h) return LBM_E_INVALID;
-    return guarded(h, [&] { h->run_steps(steps, accelerate_first != 0); });
+    return guarded(h, [&] {
+        h->run_steps(steps, accelerate_first != 0);
+        h->check_finite_after_run();
+    });
+}
+
+int lbm_nonfinite_count(lbm_handle *h, int64_t *count) {
+    if (!h || !count) return LBM_E_INVALID;
+    return guarded(h, [&] { *count = h->nonfinite_count(); });
 }
 
 int lbm_store(lbm_handle *h, float *cells_aos, float *av_vels, int32_t n_av) {

@@ -30,6 +30,8 @@
 // This is a bandwidth-bound stencil (72 algorithmic bytes per cell update,
 // ~1 flop/byte): no MFMA.
 
+#include <algorithm>
+
 #include "lbm_device.hpp"
 
 namespace lbm {
@@ -326,6 +328,27 @@ __global__ __launch_bounds__(BLOCK) void aos_to_soa(const float *aos, float *f, 
     for (int k = 0; k < Q; ++k) d[k * P] = aos[i * Q + k];
 }
 
+// LBM_NAN_CHECK / lbm_nonfinite_count: populations of the w x h interior
+// that are NaN or +-Inf (SURVEY §5 "NaN scan of f in debug mode").  One
+// 64-bit atomic per block that found any.
+__global__ __launch_bounds__(BLOCK) void count_nonfinite(const float *f, long long P, int pitch, int w, int h,
+                                                         unsigned long long *out) {
+    __shared__ unsigned blk;
+    if (threadIdx.x == 0) blk = 0;
+    __syncthreads();
+    const long long n = (long long)w * h;
+    unsigned mine = 0;
+    for (long long i = (long long)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (long long)gridDim.x * BLOCK) {
+        const long long y = i / w, x = i - y * w;
+        const float *c = f + y * pitch + x;
+#pragma unroll
+        for (int k = 0; k < Q; ++k) mine += __builtin_isfinite(c[k * P]) ? 0u : 1u;
+    }
+    if (mine) atomicAdd(&blk, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk) atomicAdd(out, (unsigned long long)blk);
+}
+
 __global__ __launch_bounds__(BLOCK) void soa_to_aos(const float *f, float *aos, long long P, int pitch, int w, int h) {
     const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= (long long)w * h) return;
@@ -476,6 +499,14 @@ hipError_t launch_init_equilibrium(float *base, long long rows, int rf, int pitc
     const long long n = rows * rf;
     hipLaunchKernelGGL(init_equilibrium, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, base, rows,
                        rf, pitch, P, c0, c1, c2);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_nonfinite(const float *f, long long P, int pitch, int w, int h, unsigned long long *out,
+                                  hipStream_t s) {
+    const long long n = (long long)w * h;
+    const unsigned blocks = (unsigned)std::min<long long>(4096, (n + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(count_nonfinite, dim3(std::max(blocks, 1u)), dim3(BLOCK), 0, s, f, P, pitch, w, h, out);
     return hipGetLastError();
 }
 

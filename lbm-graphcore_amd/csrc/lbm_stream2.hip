@@ -144,7 +144,8 @@ template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL, bool
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j,
                                              const TolK &tk, f2 *lpl) {
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
-    if (PD == 1) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
+    // (LP forms issue row j+1's loads later, at level 2: see below)
+    if (PD == 1 && !LP) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
     if (OBST) {
         const unsigned voa = st.ob[PAR][0] != 0 ? 1u : 0u, vob = st.ob[PAR][1] != 0 ? 1u : 0u;
         st.oba = (st.oba << 1) | voa;
@@ -164,6 +165,15 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
     for (int L = 1; L <= S; ++L) {
         const int b = L - 1;
         const int y = j - L;
+        if constexpr (LP && PD == 1) {
+            // LP forms: row j+1 is loaded once level 1 has consumed row j, into
+            // registers that are free by then -- one 18-VGPR row buffer
+            // instead of two; levels 2..S (>= 4 levels) cover the latency
+            if (L == 2) {
+                stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
         // pulled populations of row y (level L-1 values; x +- 1 by DPP)
         f2 s[Q];
         if constexpr (LP) {

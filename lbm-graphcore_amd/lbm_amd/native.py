@@ -34,7 +34,7 @@ EXPORTED = [
     "lbm_run", "lbm_run_steps", "lbm_store", "lbm_load_cells_local", "lbm_store_local", "lbm_local_cells",
     "lbm_last_run_seconds",
     "lbm_total_free_cells", "lbm_local_rects", "lbm_kernel_in_use", "lbm_steps_per_launch",
-    "lbm_run_stats", "lbm_placement_probe", "lbm_numerics", "lbm_source_hash",
+    "lbm_run_stats", "lbm_placement_probe", "lbm_numerics", "lbm_nonfinite_count", "lbm_source_hash",
     "lbm_last_error", "lbm_destroy",
 ]
 # every symbol include/lbm3d_hip.h declares (D3Q19 extension)
@@ -145,6 +145,7 @@ def load_library() -> ctypes.CDLL:
         "lbm_run_stats": ([H, i32p, i32p], ctypes.c_int),
         "lbm_placement_probe": ([H, i32p, i32p, f32p, i32], ctypes.c_int),
         "lbm_numerics": ([H], i32),
+        "lbm_nonfinite_count": ([H, ctypes.POINTER(i64)], ctypes.c_int),
         "lbm_last_error": ([H], ctypes.c_char_p),
         "lbm_destroy": ([H], None),
         "lbm3d_create": ([ctypes.POINTER(Params3D), u8p, ctypes.POINTER(Config), ctypes.POINTER(H)], ctypes.c_int),
@@ -333,6 +334,12 @@ class Engine:
         ms = (ctypes.c_float * 16)()
         self._check(self._L.lbm_placement_probe(self._h, ctypes.byref(kept), ctypes.byref(tried), ms, 16))
         return kept.value, [ms[i] for i in range(min(tried.value, 16))]
+
+    def nonfinite_count(self) -> int:
+        """NaN / Inf populations in the current lattice (device scan)."""
+        n = ctypes.c_int64()
+        self._check(self._L.lbm_nonfinite_count(self._h, ctypes.byref(n)))
+        return n.value
 
     def numerics(self) -> str:
         """'bitwise' (every kernel equals the CPU oracle) or 'tolerance' (LBM_FLAG_TOLERANCE collision)."""

@@ -100,3 +100,27 @@ def test_d2q9_poisoned_bitwise(gpu_lib, kw, mode):
         cells, av = e.store(n_av=11)
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=5e-5)
+
+
+def test_nonfinite_scan_and_nan_check(gpu_lib, monkeypatch):
+    """lbm_nonfinite_count (device NaN / Inf scan) and LBM_NAN_CHECK=1 (every
+    run ends with that scan and fails loudly when it finds any)."""
+    p = lio.Params(96, 40, 4, 10, 0.1, 0.005, 1.7)
+    obst = np.zeros((40, 96), np.uint8)
+    obst[0, :] = obst[-1, :] = 1
+    cells0 = lio.init_cells(p)
+    with gpu_lib.Engine(p, obst, devices=[0]) as e:
+        e.load_cells(cells0)
+        e.run_steps(4, accelerate_first=True)
+        assert e.nonfinite_count() == 0
+    bad = cells0.copy()
+    bad[17, 33, 5] = np.nan
+    bad[3, 90, 0] = np.inf
+    monkeypatch.setenv("LBM_NAN_CHECK", "1")
+    for kw in (dict(), dict(parts=4, grid=(2, 2))):
+        with gpu_lib.Engine(p, obst, devices=[0], **kw) as e:
+            e.load_cells(bad)
+            assert e.nonfinite_count() == 2
+            with pytest.raises(gpu_lib.LbmError) as ei:
+                e.run_steps(4, accelerate_first=True)
+            assert ei.value.code == gpu_lib.LBM_E_INTERNAL and "LBM_NAN_CHECK" in str(ei.value)
