@@ -289,12 +289,12 @@ struct lbm_handle {
         fused = knob("LBM_TWO_STEP", fused ? 1 : 0) != 0;
         tile2 = std::min(std::max(knob("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
         xoff = std::max(MAX_GR, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
-        stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 8);
+        stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 12);
         stream_hs = std::max(0, knob("LBM_STREAM_HS", stream_hs));
         auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
         stream_cfg = form(knob("LBM_STREAM_CFG", stream_cfg), stream_cfg);
         tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
-        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 8);
+        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 12);
         stream_min_cells = std::max(0, knob("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
             const char *g = knob_str("LBM_STREAM_GUIDE");
@@ -855,12 +855,14 @@ struct lbm_handle {
         // launch form: the tolerance collision has forms 0 and 4 only
         if (tolerance) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
         // the v3 kernel takes up to 6 steps per launch (8 in the LP form)
-        const int s_max = stream_cfg == 4 ? 8 : 6;
+        const int s_max = stream_cfg == 4 ? 12 : 6;
         const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch
                                                : std::min(tolerance ? tol_s : stream_s, s_max);
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max));
-        if (stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5..8
+        if (stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5..10 and 12
+        if (stream_cfg == 4 && S == 11)
+            throw lbm_failure(LBM_E_INVALID, "steps_per_launch 11 has no stream kernel form (5..10 or 12)");
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;
