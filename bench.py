@@ -336,11 +336,11 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
                     "that basis); parity unpinned upstream (no 3-D reference)"}
 
 
-def multi_rank_check(rank: int, world: int, local_rank: int, n: int = 2048, steps: int = 11) -> dict:
+def multi_rank_check(rank: int, world: int, local_rank: int, n: int = 2048, steps: int = 13) -> dict:
     """N > 1, untimed, before the timed region: the fused stream kernel over all
     ranks (RCCL halos, the reference partitionForIpus blocks and N x 1 slabs)
-    on an n^2 problem with random obstacles and a perturbed initial state, 11
-    steps (two fused 5-step launches + a one-step remainder), gathered on rank
+    on an n^2 problem with random obstacles and a perturbed initial state, 13
+    steps (two fused 6-step launches + a one-step remainder), gathered on rank
     0 and compared bitwise with a single-domain run of the same library on
     rank 0's GPU (which tests/test_gpu_parity.py pins to the CPU oracle).
     Reference: StructuredGridUtils.hpp:498-522 (split), :805-851 (halos)."""
@@ -494,7 +494,7 @@ def main() -> int:
     ap.add_argument("--kernel", default="auto", choices=["auto", "resident", "stream", "step2", "vec4", "scalar", "pipeline"],
                     help="stream: fused S-step register-streaming kernel; step2: fused two-step LDS kernel; "
                          "vec4/scalar: one step per launch; auto: the library's choice")
-    ap.add_argument("--spl", type=int, default=0, help="stream: time steps per launch (2..6; 0 = library default, 5)")
+    ap.add_argument("--spl", type=int, default=0, help="stream: time steps per launch (2..6; 0 = library default, 6)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true")
     ap.add_argument("--no-d3q19", action="store_true")

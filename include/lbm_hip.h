@@ -56,7 +56,7 @@ typedef struct lbm_params {
 enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
 /* Step kernels.  SCALAR / VEC4: one time step per launch (VEC4 needs widths
  * that are multiples of 4).  STEP2: fused two-step launches through LDS.
- * STREAM: fused S-step launches (S = steps_per_launch, 2..6; default 5) streaming rows
+ * STREAM: fused S-step launches (S = steps_per_launch, 2..6; default 6) streaming rows
  * through registers.  RESIDENT: every step of a run in one persistent
  * launch with the lattice held on chip (LDS + registers) -- single
  * sub-domain grids small enough for all of their 64-column tiles to be
@@ -106,7 +106,7 @@ typedef struct lbm_config {
     int32_t graph_steps;    /* >0: replay the step loop as hipGraphs of 2*graph_steps steps
                                (single sub-domain without exchange); <0: off; 0: library default */
     int32_t flags;          /* LBM_FLAG_* */
-    int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..6); 0 = library default (5) */
+    int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..6); 0 = library default (6) */
 } lbm_config;
 
 /* Route the periodic wrap of undecomposed dimensions through the transport

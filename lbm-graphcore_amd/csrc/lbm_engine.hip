@@ -192,13 +192,13 @@ struct lbm_handle {
     int spl = 2;             // steps per fused launch
     int hw = 2;              // WG halo width (= spl)
     int gr = 2;              // ghost ring width
-    int stream_s = 5;        // LBM_STREAM_S: steps per stream launch when not configured (v1 / v2 kernels: at most 4)
+    int stream_s = 6;        // LBM_STREAM_S: steps per stream launch when not configured
     int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
     int og = 4;              // ghost width of the obstacle map
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
-    int stream_cfg = 0;      // LBM_STREAM_CFG (v3 launch form, one wave per workgroup): 0 plain stores;
+    int stream_cfg = 4;      // LBM_STREAM_CFG (launch form, one wave per workgroup): 0 plain stores;
                              // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 8)
-    int tol_s = 5, tol_cfg = 0;  // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
+    int tol_s = 6, tol_cfg = 4;  // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
@@ -289,12 +289,12 @@ struct lbm_handle {
         fused = knob("LBM_TWO_STEP", fused ? 1 : 0) != 0;
         tile2 = std::min(std::max(knob("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
         xoff = std::max(MAX_GR, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
-        stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 12);
+        stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 6);
         stream_hs = std::max(0, knob("LBM_STREAM_HS", stream_hs));
         auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
         stream_cfg = form(knob("LBM_STREAM_CFG", stream_cfg), stream_cfg);
         tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
-        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 12);
+        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 6);
         stream_min_cells = std::max(0, knob("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
             const char *g = knob_str("LBM_STREAM_GUIDE");
@@ -855,14 +855,12 @@ struct lbm_handle {
         // launch form: the tolerance collision has forms 0 and 4 only
         if (tolerance) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
         // the v3 kernel takes up to 6 steps per launch (8 in the LP form)
-        const int s_max = stream_cfg == 4 ? 12 : 6;
+        const int s_max = 6;
         const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch
                                                : std::min(tolerance ? tol_s : stream_s, s_max);
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max));
-        if (stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5..10 and 12
-        if (stream_cfg == 4 && S == 11)
-            throw lbm_failure(LBM_E_INVALID, "steps_per_launch 11 has no stream kernel form (5..10 or 12)");
+        if (stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5, 6
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;

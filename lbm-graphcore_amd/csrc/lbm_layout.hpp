@@ -34,7 +34,7 @@ namespace lbm {
 
 constexpr int Q = 9;
 constexpr int XOFF = 4;   // interior column 0 offset inside a plane row
-constexpr int MAX_GR = 12;  // widest ghost ring (rows/columns) any kernel needs (stream kernel LP form, S <= 12)
+constexpr int MAX_GR = 6;  // widest ghost ring (rows/columns) any kernel needs (stream kernel, S <= 6)
 constexpr int BLOCK = 256;  // 4 wave64s
 constexpr int MAX_RECTS = 4;
 constexpr int MAX_SRECTS = 32;  // stream kernels: guided per-XCD row bands (lbm_engine.hip stream_split)

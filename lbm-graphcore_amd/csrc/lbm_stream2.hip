@@ -347,11 +347,13 @@ __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, 
 // (A persistent grid taking units from a device-scope counter balanced the
 // waves better but read 1.30x the algorithmic bytes instead of 1.18x:
 // neighbouring strips landed on different XCDs.)
-// Register budget: two waves per SIMD (256 VGPRs each) up to S = 6; the LP
-// forms with S >= 7 run one wave per SIMD, whose 512 registers (VGPRs plus
-// AGPRs as spill space) hold the deeper level state without scratch.
+// Two waves per SIMD (256 VGPRs each).  Deeper LP forms were measured and
+// removed: at two waves per SIMD S >= 7 spills (41-63 VGPRs), at one wave per
+// SIMD (AGPRs as spill space, no scratch) S = 7..12 ran 175-214 GLUPS
+// bitwise and 263-314 tolerance against 290 / 333 for S = 6
+// (profiles/r03/ab_lp_depth.log).
 template <int S, bool kReduce, int W, bool NT, bool TOL = false, bool LP = false>
-__global__ __launch_bounds__(64 * W, (LP && S >= 7) ? 1 : 2) void stream_steps2d(StreamArgs a) {
+__global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     __shared__ float lds[W];
     __shared__ f2 lds_p[LP ? W * 3 * S * 64 : 1];  // LP: [wave][S][3][64]
     if (kReduce && blockIdx.x == 0) reduce_pending_n<64 * W>(a.ctl, a.partials_prev, a.av_local, lds);
@@ -411,11 +413,6 @@ hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, h
         case 4: hipLaunchKernelGGL(stream2d_flags<4>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 5: hipLaunchKernelGGL(stream2d_flags<5>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 6: hipLaunchKernelGGL(stream2d_flags<6>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
-        case 7: hipLaunchKernelGGL(stream2d_flags<7>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
-        case 8: hipLaunchKernelGGL(stream2d_flags<8>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
-        case 9: hipLaunchKernelGGL(stream2d_flags<9>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
-        case 10: hipLaunchKernelGGL(stream2d_flags<10>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
-        case 12: hipLaunchKernelGGL(stream2d_flags<12>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -437,10 +434,10 @@ static const void *s2d_fn() {
 // Launch forms (cfg; one wave per workgroup in all of them -- four-wave
 // workgroups on adjacent strips lost their A/B, profiles/r02/ab_cfg_s5.log):
 //   0 plain stores, 3 non-temporal lattice stores, 4 LP (older rows of
-//   planes 2, 5, 6 in LDS; S = 5..10 and 12).
+//   planes 2, 5, 6 in LDS; S = 5, 6: the default, S = 6).
 // tol: the LBM_FLAG_TOLERANCE collision (collide2t) in forms 0 and 4.
 static bool s2d_form_ok(int steps, int cfg, bool tol) {
-    if (cfg == 4) return steps >= 5 && (steps <= 10 || steps == 12);
+    if (cfg == 4) return steps >= 5 && steps <= 6;
     if (cfg == 0) return steps >= 2 && steps <= 6;
     if (cfg == 3) return !tol && steps >= 2 && steps <= 6;
     return false;
@@ -454,12 +451,7 @@ hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
     if (cfg == 4) {
         switch (steps) {
             case 5: fn = tol ? s2d_fn<5, true, true>() : s2d_fn<5, false, true>(); break;
-            case 6: fn = tol ? s2d_fn<6, true, true>() : s2d_fn<6, false, true>(); break;
-            case 7: fn = tol ? s2d_fn<7, true, true>() : s2d_fn<7, false, true>(); break;
-            case 8: fn = tol ? s2d_fn<8, true, true>() : s2d_fn<8, false, true>(); break;
-            case 9: fn = tol ? s2d_fn<9, true, true>() : s2d_fn<9, false, true>(); break;
-            case 10: fn = tol ? s2d_fn<10, true, true>() : s2d_fn<10, false, true>(); break;
-            default: fn = tol ? s2d_fn<12, true, true>() : s2d_fn<12, false, true>(); break;
+            default: fn = tol ? s2d_fn<6, true, true>() : s2d_fn<6, false, true>(); break;
         }
     } else {  // cfg 3 has the registers of cfg 0
         switch (steps) {
@@ -481,16 +473,6 @@ hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduc
             case 11: launch_s2d<5, false, true, true>(a, units, reduce, s); break;
             case 12: launch_s2d<6, false, false, true>(a, units, reduce, s); break;
             case 13: launch_s2d<6, false, true, true>(a, units, reduce, s); break;
-            case 14: launch_s2d<7, false, false, true>(a, units, reduce, s); break;
-            case 15: launch_s2d<7, false, true, true>(a, units, reduce, s); break;
-            case 16: launch_s2d<8, false, false, true>(a, units, reduce, s); break;
-            case 17: launch_s2d<8, false, true, true>(a, units, reduce, s); break;
-            case 18: launch_s2d<9, false, false, true>(a, units, reduce, s); break;
-            case 19: launch_s2d<9, false, true, true>(a, units, reduce, s); break;
-            case 20: launch_s2d<10, false, false, true>(a, units, reduce, s); break;
-            case 21: launch_s2d<10, false, true, true>(a, units, reduce, s); break;
-            case 24: launch_s2d<12, false, false, true>(a, units, reduce, s); break;
-            case 25: launch_s2d<12, false, true, true>(a, units, reduce, s); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

@@ -36,7 +36,7 @@ void usage(const char *exe) {
               << "      --runs arg       timed re-runs after the first (default: 5)\n"
               << "      --kernel arg     auto, resident, stream, step2, vec4, scalar or pipeline (default: auto; vec4/scalar = one\n"
               << "                       step per launch; pipeline = unfused per-stage kernels)\n"
-              << "      --spl arg        stream kernel: time steps per launch, 2..4 (default: library choice)\n"
+              << "      --spl arg        stream kernel: time steps per launch, 2..6 (default: library choice, 6)\n"
               << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n"
               << "      --graph-steps arg  replay the step loop as hipGraphs of 2*arg launches (0 = library default, <0 = off)\n"
               << "      --dump-partitioning arg  write the sub-domain decomposition as JSON\n";

@@ -1,7 +1,7 @@
 """One rank of tests/test_multigpu.py (started as a fresh process per GPU; the
 parent never initialises HIP).  RCCL-transport engine with the fused stream
-kernel (S = 5) on a 2048^2 problem (random obstacles, perturbed start), 11
-steps = two fused launches + a one-step remainder, per-rank load/store of the
+kernel (LP form, S = 6) on a 2048^2 problem (random obstacles, perturbed
+start), 13 steps = two fused launches + a one-step remainder, per-rank load/store of the
 rank's own block; rank 0 gathers the blocks over gloo and compares the
 lattice bitwise with the CPU oracle (LastChance.cpp:192-266 restated).
 Decompositions: the reference partitionForIpus rule
@@ -30,7 +30,7 @@ def main() -> int:
     import torch.distributed as dist
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    n, steps = 2048, 11
+    n, steps = 2048, 13
     rng = np.random.default_rng(77)
     p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
     obst = np.zeros((n, n), np.uint8)

@@ -6,9 +6,8 @@ equal to a single-domain run of the same engine (and finite).
 
   * 16384^2 (config 4) as 8 sub-domains: the reference's 2x4 blocks
     (partitionForIpus for 8 on a square grid, StructuredGridUtils.hpp:498-522)
-    and 8x1 y slabs; 8 steps (one 5-step stream launch + three one-step
-    launches, W1 halo, WG refresh) then 6 more (one fused launch + one one-step
-    launch);
+    and 8x1 y slabs; 8 steps (one 6-step stream launch + two one-step
+    launches, W1 halo, WG refresh) then 6 more (one fused launch);
   * D3Q19 512^3 (config 5) as 8 z slabs against one slab (parity of the 3-D
     model is unpinned upstream: there is no 3-D reference code).
 

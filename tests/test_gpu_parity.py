@@ -216,28 +216,27 @@ def bench_obstacles(n):
 
 @pytest.mark.parametrize("mode", ["step2", "stream4", "stream5", "auto"])
 def test_large_grid_steps_and_conservation(gpu_lib, mode):
-    """8192^2 (the roofline config, BASELINE config 3): 11 steps bitwise vs the
-    oracle -- for the headline kernel (auto = stream, S = 5, default guide
-    tiers, per-unit obstacle flags, XCD unit permutation, placement probe on)
-    that is two fused 5-step launches plus a one-step remainder, and the test
-    asserts the fused launches ran -- then mass conserved over 200 steps.
-    Reference work unit: LastChance.cpp:192-266."""
+    """8192^2 (the roofline config, BASELINE config 3): 2S + 1 steps bitwise
+    vs the oracle -- for the headline kernel (auto = stream, LP form, S = 6,
+    default guide tiers, per-unit obstacle flags, XCD unit permutation,
+    placement probe on) that is two fused 6-step launches plus a one-step
+    remainder, and the test asserts the fused launches ran -- then mass
+    conserved over 200 steps.  Reference work unit: LastChance.cpp:192-266."""
     n = 8192
-    p = lio.Params(n, n, 11, 10, 0.1, 0.005, 1.85)
+    S = {"step2": 2, "stream4": 4, "stream5": 5, "auto": 6}[mode]
+    steps = 2 * S + 1
+    p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
     obst = bench_obstacles(n)
     cells0 = lio.init_cells(p)
-    ref, ref_av = oracle.run_mt(p, obst, 11, 16, cells0)
+    ref, ref_av = oracle.run_mt(p, obst, steps, 16, cells0)
     kw = {} if mode == "auto" else mode_kw(gpu_lib, mode)
     with gpu_lib.Engine(p, obst, **kw) as e:
         assert e.kernel_in_use() == ("stream" if mode == "auto" else kname(mode))
-        spl = e.steps_per_launch()
-        if mode in ("auto", "stream5"):
-            assert spl == 5
+        assert e.steps_per_launch() == S
         e.init_equilibrium()
-        e.run_steps(11, accelerate_first=True)
-        fused, single = e.run_stats()
-        assert (fused, single) == (11 // spl, 11 % spl) and fused >= 1
-        cells, av = e.store(n_av=11)
+        e.run_steps(steps, accelerate_first=True)
+        assert e.run_stats() == (2, 1)
+        cells, av = e.store(n_av=steps)
         assert np.array_equal(cells, ref)
         # the oracle sums 67M |u| terms sequentially in fp32 (~sqrt(n)*eps ~ 5e-4
         # relative drift); the GPU sums in trees
@@ -314,7 +313,7 @@ def test_step2_tile_variants_bitwise(gpu_lib, tile, monkeypatch):
     np.testing.assert_allclose(av, r2av, rtol=1e-5)
 
 
-@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (5, 4), (7, 4), (8, 4)])
+@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (5, 4), (6, 4)])
 @pytest.mark.parametrize("hs", [1, 7, 100000])
 def test_stream_segments_bitwise(gpu_lib, S, cfg, hs, monkeypatch):
     """The stream kernel (plain and LP launch forms) with segment heights from
@@ -337,19 +336,19 @@ def test_stream_segments_bitwise(gpu_lib, S, cfg, hs, monkeypatch):
 
 def test_16384_single_domain_vs_oracle(gpu_lib):
     """BASELINE config 4's grid on one GPU with the headline kernel (auto =
-    stream, S = 5, placement probe on): 6 steps = one fused 5-step launch +
-    one one-step launch, bitwise vs the oracle (OpenMP restatement, the same
-    lattice as oracle.run) over the full 16384^2 lattice."""
+    stream, LP form, S = 6, placement probe on): 7 steps = one fused 6-step
+    launch + one one-step launch, bitwise vs the oracle (OpenMP restatement,
+    the same lattice as oracle.run) over the full 16384^2 lattice."""
     n = 16384
-    p = lio.Params(n, n, 6, 10, 0.1, 0.005, 1.85)
+    p = lio.Params(n, n, 7, 10, 0.1, 0.005, 1.85)
     obst = bench_obstacles(n)
     with gpu_lib.Engine(p, obst) as e:
-        assert e.kernel_in_use() == "stream" and e.steps_per_launch() == 5
+        assert e.kernel_in_use() == "stream" and e.steps_per_launch() == 6
         e.init_equilibrium()
-        e.run_steps(6, accelerate_first=True)
+        e.run_steps(7, accelerate_first=True)
         assert e.run_stats() == (1, 1)
-        cells, av = e.store(n_av=6)
-    ref, ref_av = oracle.run_mt(p, obst, 6, 16, lio.init_cells(p))
+        cells, av = e.store(n_av=7)
+    ref, ref_av = oracle.run_mt(p, obst, 7, 16, lio.init_cells(p))
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=5e-3)  # 268M-term sequential fp32 sums in the oracle
 
@@ -359,10 +358,10 @@ def test_16384_lattice_64bit_indexing(gpu_lib):
     2^31): every index into it must be 64-bit.  (The one-step kernels' ghost-edge
     stores once formed y * pitch in 32 bits and faulted there -- reached by the
     remainder of a step count that is not a multiple of the stream kernel's S.)
-    6 steps = one 5-step stream launch + one one-step launch, against six
+    7 steps = one 6-step stream launch + one one-step launch, against seven
     one-step (vec4) launches: bitwise equal and finite."""
     n = 16384
-    p = lio.Params(n, n, 6, 10, 0.1, 0.005, 1.85)
+    p = lio.Params(n, n, 7, 10, 0.1, 0.005, 1.85)
     obst = np.zeros((n, n), np.uint8)
     obst[0, :] = obst[-1, :] = 1
     obst[:, n // 3] = 1
@@ -370,8 +369,8 @@ def test_16384_lattice_64bit_indexing(gpu_lib):
     for name, kw in (("auto", {}), ("vec4", mode_kw(gpu_lib, "vec4"))):
         with gpu_lib.Engine(p, obst, **kw) as e:
             e.init_equilibrium()
-            e.run_steps(6, accelerate_first=True)
-            runs[name] = (e.kernel_in_use(), *e.store(n_av=6))
+            e.run_steps(7, accelerate_first=True)
+            runs[name] = (e.kernel_in_use(), *e.store(n_av=7))
     assert runs["auto"][0] == "stream" and runs["vec4"][0] == "vec4"
     a, b = runs["auto"][1], runs["vec4"][1]
     assert np.isfinite(a[:: 97, :: 89]).all()
@@ -397,7 +396,7 @@ def test_stream_size_limits(gpu_lib):
         assert e.kernel_in_use() in ("step2", "stream")
 
 
-@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5", "stream6", "lp7", "lp8"])
+@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5", "stream6", "lp5", "lp6"])
 def test_open_periodic_random_bitwise(gpu_lib, mode, monkeypatch):
     """No walls: flow crosses every periodic seam and every sub-domain seam.
     Random sparse obstacles, perturbed populations, odd sizes; single domain
@@ -537,7 +536,7 @@ def test_pipeline_reference_grid_full_run(gpu_lib, grid, tmp_path):
 # ------------------------------------- wide decomposed x bands (stream) ----
 
 @pytest.mark.parametrize("nx", [1030, 1031])
-@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 4), (8, 4)])
+@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (5, 4), (6, 4)])
 def test_stream_wide_x_bands_bitwise(gpu_lib, nx, S, cfg, monkeypatch):
     """Sub-domains wide enough (>= 4 strips) for the strip-wide x boundary band
     of a decomposed x side (lbm_engine.hip stream_split: xb = one strip, the
@@ -581,7 +580,7 @@ def _adversarial_state(nx, ny, seed):
     return cells.astype(np.float32)
 
 
-@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp8", "resident", "vec4", "step2"])
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp6", "resident", "vec4", "step2"])
 def test_division_adversarial_states_bitwise(gpu_lib, mode, monkeypatch):
     """lbm_packed.hpp's short division sequences (x/9, x/36 by multiply + two
     corrections; n/rho without v_div_scale / v_div_fixup) against the oracle's
@@ -609,7 +608,7 @@ def test_division_adversarial_states_bitwise(gpu_lib, mode, monkeypatch):
                         f"gpu {cells[y, x, k]!r} oracle {ref[y, x, k]!r}")
 
 
-@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp8", "resident", "vec4", "step2"])
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp6", "resident", "vec4", "step2"])
 def test_signed_zero_states_bitwise(gpu_lib, mode, monkeypatch):
     """The folded acceleration is added on EVERY row as accel * w
     (LastChance.cpp:253-261: + 0 * w1 off the accelerated row), which turns a
@@ -667,11 +666,11 @@ def test_local_load_store_matches_full(gpu_lib, parts, grid):
     assert np.array_equal(av, av_full)
 
 
-@pytest.mark.parametrize("S,cfg", [(4, 0), (5, 0), (6, 0), (4, 3), (5, 3), (6, 3), (5, 4), (6, 4), (7, 4), (8, 4)])
+@pytest.mark.parametrize("S,cfg", [(4, 0), (5, 0), (6, 0), (4, 3), (5, 3), (6, 3), (5, 4), (6, 4)])
 def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, S, monkeypatch):
     """The stream kernel's launch forms (LBM_STREAM_CFG: 0 plain stores, 3
-    non-temporal lattice stores, 4 LP: older plane rows in LDS, up to 8 steps
-    per launch) and its guided segment tiers: bitwise vs the oracle on a
+    non-temporal lattice stores, 4 LP: older plane rows in LDS, the default
+    form) and its guided segment tiers: bitwise vs the oracle on a
     single domain, 2x2 and 1x3 loop-back, and with one-step remainders."""
     monkeypatch.setenv("LBM_STREAM_CFG", str(cfg))
     monkeypatch.setenv("LBM_STREAM_GUIDE", "24:0.6,8:0.3,3")
@@ -712,8 +711,8 @@ def test_lattice_placement_knobs_bitwise(gpu_lib, env, monkeypatch):
 def test_placement_probe_same_lattice(gpu_lib, transport, monkeypatch):
     """The placement probe (8192x4096 = 2^25 cells, the
     smallest sub-domain it runs on) leaves the engine as if it had not run:
-    lattice and av_vels bitwise equal with and without it, 11 steps (two
-    5-step launches and a one-step remainder); also as a one-rank RCCL block
+    lattice and av_vels bitwise equal with and without it, 13 steps (two
+    6-step launches and a one-step remainder); also as a one-rank RCCL block
     whose periodic wraps go through self send/recv."""
     p = lio.Params(8192, 4096, 0, 11, 0.1, 0.005, 1.7)
     obst = np.zeros((p.ny, p.nx), np.uint8)
@@ -736,8 +735,9 @@ def test_placement_probe_same_lattice(gpu_lib, transport, monkeypatch):
             assert (kept, len(ms)) == ((-1, 0) if tries == "1" else (2, 3))
             assert e.kernel_in_use() == "stream"
             e.load_cells(cells0)
-            e.run_steps(11, accelerate_first=True)
-            out.append(e.store(n_av=11))
+            e.run_steps(13, accelerate_first=True)
+            assert e.run_stats() == (2, 1)
+            out.append(e.store(n_av=13))
     assert np.array_equal(out[0][0], out[1][0])
     assert np.array_equal(out[0][1], out[1][1])
     assert np.isfinite(out[1][1]).all()
