@@ -378,6 +378,23 @@ def multi_rank_check(rank: int, world: int, local_rank: int, n: int = 2048, step
     return {"passed": bool(ok[0]), "grid": f"{n}x{n}", "steps": steps, "cases": results}
 
 
+# Device ms per launch at 8192^2 (profiles/r03/): fused 6-step and 5-step
+# stream launches, and the one-step launch a remainder of K % S steps costs.
+LAUNCH_MS = {6: 1.41, 5: 1.22, 1: 0.81}
+
+
+def pick_spl(steps: int, requested: int) -> int:
+    """Steps per fused launch for a timed run of `steps` steps: the caller's
+    choice if given, else whichever of the library's two fastest forms (S = 6,
+    S = 5) finishes `steps` sooner once the one-step launches of a remainder
+    (steps % S) are counted -- the driver's 20-step run is four 5-step
+    launches, a 1000-step run 166 six-step launches plus four one-step ones."""
+    if requested:
+        return requested
+    est = {S: (steps // S) * LAUNCH_MS[S] + (steps % S) * LAUNCH_MS[1] for S in (6, 5)}
+    return min(est, key=lambda S: (est[S], -S))
+
+
 def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: int, rank: int, world: int,
                  local_rank: int, dist_on: bool) -> dict:
     """K timed steps of the weak-scaling workload: R x C tiles of tnx x tny cells,
@@ -395,7 +412,8 @@ def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: 
     eng = native.Engine(p, obst, parts=world, grid=(R, C),
                         transport=native.TRANSPORT_RCCL if dist_on else native.TRANSPORT_LOCAL,
                         rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel, flags=kflags,
-                        steps_per_launch=args.spl)
+                        steps_per_launch=pick_spl(args.steps, args.spl) if kernel in (native.KERNEL_AUTO,
+                                                                                       native.KERNEL_STREAM) else args.spl)
     try:
         eng.init_equilibrium()
         spl = eng.steps_per_launch()
