@@ -860,7 +860,7 @@ struct lbm_handle {
                                                : std::min(tolerance ? tol_s : stream_s, s_max);
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max));
-        if (stream_cfg == 4 && S < 5) stream_cfg = 0;  // LP forms exist for S = 5, 6
+        if (stream_cfg == 4 && S != 6) stream_cfg = 0;  // the LP form exists for S = 6 (below it: no gain)
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;

@@ -434,10 +434,12 @@ static const void *s2d_fn() {
 // Launch forms (cfg; one wave per workgroup in all of them -- four-wave
 // workgroups on adjacent strips lost their A/B, profiles/r02/ab_cfg_s5.log):
 //   0 plain stores, 3 non-temporal lattice stores, 4 LP (older rows of
-//   planes 2, 5, 6 in LDS; S = 5, 6: the default, S = 6).
+//   planes 2, 5, 6 in LDS; S = 6 only: the default form at S = 6, where the
+//   plain form runs out of registers; at S = 5 the two forms measure equal,
+//   profiles/r03/ab_forms_s5_s6.log).
 // tol: the LBM_FLAG_TOLERANCE collision (collide2t) in forms 0 and 4.
 static bool s2d_form_ok(int steps, int cfg, bool tol) {
-    if (cfg == 4) return steps >= 5 && steps <= 6;
+    if (cfg == 4) return steps == 6;
     if (cfg == 0) return steps >= 2 && steps <= 6;
     if (cfg == 3) return !tol && steps >= 2 && steps <= 6;
     return false;
@@ -450,7 +452,6 @@ hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
     const void *fn = nullptr;
     if (cfg == 4) {
         switch (steps) {
-            case 5: fn = tol ? s2d_fn<5, true, true>() : s2d_fn<5, false, true>(); break;
             default: fn = tol ? s2d_fn<6, true, true>() : s2d_fn<6, false, true>(); break;
         }
     } else {  // cfg 3 has the registers of cfg 0
@@ -469,8 +470,6 @@ hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduc
     if (!s2d_form_ok(steps, cfg, tol)) return hipErrorInvalidValue;
     if (cfg == 4) {
         switch (steps * 2 + (tol ? 1 : 0)) {
-            case 10: launch_s2d<5, false, false, true>(a, units, reduce, s); break;
-            case 11: launch_s2d<5, false, true, true>(a, units, reduce, s); break;
             case 12: launch_s2d<6, false, false, true>(a, units, reduce, s); break;
             case 13: launch_s2d<6, false, true, true>(a, units, reduce, s); break;
             default: return hipErrorInvalidValue;

@@ -313,7 +313,7 @@ def test_step2_tile_variants_bitwise(gpu_lib, tile, monkeypatch):
     np.testing.assert_allclose(av, r2av, rtol=1e-5)
 
 
-@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (5, 4), (6, 4)])
+@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (6, 4)])
 @pytest.mark.parametrize("hs", [1, 7, 100000])
 def test_stream_segments_bitwise(gpu_lib, S, cfg, hs, monkeypatch):
     """The stream kernel (plain and LP launch forms) with segment heights from
@@ -396,14 +396,14 @@ def test_stream_size_limits(gpu_lib):
         assert e.kernel_in_use() in ("step2", "stream")
 
 
-@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5", "stream6", "lp5", "lp6"])
+@pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5", "stream6", "plain6"])
 def test_open_periodic_random_bitwise(gpu_lib, mode, monkeypatch):
     """No walls: flow crosses every periodic seam and every sub-domain seam.
     Random sparse obstacles, perturbed populations, odd sizes; single domain
     and 2x2 / 3x2 loop-back decompositions."""
-    if mode.startswith("lp"):  # LP launch form (LBM_STREAM_CFG=4)
-        monkeypatch.setenv("LBM_STREAM_CFG", "4")
-        mode = "stream" + mode[2:]
+    if mode.startswith("plain"):  # S = 6 in the plain form (the default S = 6 form is LP)
+        monkeypatch.setenv("LBM_STREAM_CFG", "0")
+        mode = "stream" + mode[5:]
     rng = np.random.default_rng(7)
     p = lio.Params(150, 70, 9, 10, 0.1, 0.02, 1.7)
     obst = (rng.random((70, 150)) < 0.05).astype(np.uint8)
@@ -536,7 +536,7 @@ def test_pipeline_reference_grid_full_run(gpu_lib, grid, tmp_path):
 # ------------------------------------- wide decomposed x bands (stream) ----
 
 @pytest.mark.parametrize("nx", [1030, 1031])
-@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (5, 4), (6, 4)])
+@pytest.mark.parametrize("S,cfg", [(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (6, 4)])
 def test_stream_wide_x_bands_bitwise(gpu_lib, nx, S, cfg, monkeypatch):
     """Sub-domains wide enough (>= 4 strips) for the strip-wide x boundary band
     of a decomposed x side (lbm_engine.hip stream_split: xb = one strip, the
@@ -580,7 +580,7 @@ def _adversarial_state(nx, ny, seed):
     return cells.astype(np.float32)
 
 
-@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp6", "resident", "vec4", "step2"])
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "stream6", "plain6", "resident", "vec4", "step2"])
 def test_division_adversarial_states_bitwise(gpu_lib, mode, monkeypatch):
     """lbm_packed.hpp's short division sequences (x/9, x/36 by multiply + two
     corrections; n/rho without v_div_scale / v_div_fixup) against the oracle's
@@ -588,9 +588,9 @@ def test_division_adversarial_states_bitwise(gpu_lib, mode, monkeypatch):
     tiny normal or subnormal and rho spans many binades (down to the smallest
     normals): the lattice must stay bitwise equal.  One step and three steps,
     no obstacles and no acceleration (so the states stay in their binades)."""
-    if mode.startswith("lp"):
-        monkeypatch.setenv("LBM_STREAM_CFG", "4")
-        mode = "stream" + mode[2:]
+    if mode.startswith("plain"):  # S = 6 in the plain form (the default S = 6 form is LP)
+        monkeypatch.setenv("LBM_STREAM_CFG", "0")
+        mode = "stream" + mode[5:]
     monkeypatch.setenv("LBM_RES_V", "2")  # the packed resident kernel (collide2)
     nx, ny = 256, 66
     p = lio.Params(nx, ny, 3, 10, 0.1, 0.0, 1.85)
@@ -608,7 +608,7 @@ def test_division_adversarial_states_bitwise(gpu_lib, mode, monkeypatch):
                         f"gpu {cells[y, x, k]!r} oracle {ref[y, x, k]!r}")
 
 
-@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "lp5", "lp6", "resident", "vec4", "step2"])
+@pytest.mark.parametrize("mode", ["stream2", "stream3", "stream4", "stream5", "stream6", "plain6", "resident", "vec4", "step2"])
 def test_signed_zero_states_bitwise(gpu_lib, mode, monkeypatch):
     """The folded acceleration is added on EVERY row as accel * w
     (LastChance.cpp:253-261: + 0 * w1 off the accelerated row), which turns a
@@ -617,9 +617,9 @@ def test_signed_zero_states_bitwise(gpu_lib, mode, monkeypatch):
     produces -0.0 populations on every row; a kernel that skipped the add off
     the accelerated row would keep them negative.  Bitwise vs the oracle,
     NaN positions equal (their payloads are not compared)."""
-    if mode.startswith("lp"):
-        monkeypatch.setenv("LBM_STREAM_CFG", "4")
-        mode = "stream" + mode[2:]
+    if mode.startswith("plain"):  # S = 6 in the plain form (the default S = 6 form is LP)
+        monkeypatch.setenv("LBM_STREAM_CFG", "0")
+        mode = "stream" + mode[5:]
     monkeypatch.setenv("LBM_RES_V", "2")
     nx, ny = 256, 66
     p = lio.Params(nx, ny, 3, 10, 0.1, 0.005, 1.85)
@@ -666,7 +666,7 @@ def test_local_load_store_matches_full(gpu_lib, parts, grid):
     assert np.array_equal(av, av_full)
 
 
-@pytest.mark.parametrize("S,cfg", [(4, 0), (5, 0), (6, 0), (4, 3), (5, 3), (6, 3), (5, 4), (6, 4)])
+@pytest.mark.parametrize("S,cfg", [(4, 0), (5, 0), (6, 0), (4, 3), (5, 3), (6, 3), (6, 4)])
 def test_stream_v3_launch_configs_bitwise(gpu_lib, cfg, S, monkeypatch):
     """The stream kernel's launch forms (LBM_STREAM_CFG: 0 plain stores, 3
     non-temporal lattice stores, 4 LP: older plane rows in LDS, the default
