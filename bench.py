@@ -220,11 +220,12 @@ def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
         e.run()                      # timed re-run (device events), as LbmRunner's readTimer runs
         secs = e.last_run_seconds()
         used = e.kernel_in_use()
+        numerics = e.numerics()
     cells = p.nx * p.ny
     note = ("lattice held on chip (LDS) for the whole run by the resident kernel: bound by the per-step "
             "neighbour hand-off and the collision, not by HBM" if used == "resident" else
             "lattice pair (151 MB) fits the 256 MB Infinity Cache: not an HBM-roofline number")
-    return {"grid": "1024x1024", "steps": p.max_iters, "kernel": used,
+    return {"grid": "1024x1024", "steps": p.max_iters, "kernel": used, "numerics": numerics,
             "mlups": round(cells * p.max_iters / secs / 1e6, 1),
             "ms_per_step": round(secs / p.max_iters * 1e3, 5),
             "reynolds": lio.reynolds_number(p, float(av[-1])), "note": note}
@@ -651,6 +652,10 @@ def main() -> int:
                 aux["config2_1024x1024"] = aux_1024(kernel, kflags, args.spl)
             except Exception as exc:
                 aux["config2_1024x1024"] = {"error": str(exc)}
+            try:  # the same problem with LBM_FLAG_TOLERANCE (packed resident tiles, reciprocal collision)
+                aux["config2_1024x1024_tolerance"] = aux_1024(kernel, kflags | native.FLAG_TOLERANCE, args.spl)
+            except Exception as exc:
+                aux["config2_1024x1024_tolerance"] = {"error": str(exc)}
         if not args.no_cpu_baseline:
             for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_config1_128x128", cpu_config1),
                             ("cpu_lastchance_1024x1024", cpu_lastchance_1024),

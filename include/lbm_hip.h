@@ -122,8 +122,10 @@ typedef struct lbm_config {
  * multiplications, and FMA contraction.  Still IEEE fp32 arithmetic, but no
  * longer bitwise equal to LastChance.cpp:226-262: after 100 steps at 8192^2
  * every population stays within 2e-6 relative of the oracle, and check.py
- * passes on all four reference grids (tests/test_gpu_tolerance.py).  Other
- * kernels (remainder one-step launches, RESIDENT, STEP2) stay bitwise.
+ * passes on all four reference grids (tests/test_gpu_tolerance.py).  The
+ * packed RESIDENT tiles take the same collision; the other kernels
+ * (remainder one-step launches, STEP2, VEC4, the scalar resident tiles) stay
+ * bitwise.
  * lbm_numerics() reports which mode a handle runs. */
 #define LBM_FLAG_TOLERANCE 4
 

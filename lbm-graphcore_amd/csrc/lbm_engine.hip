@@ -58,7 +58,7 @@ hipError_t launch_count_nonfinite(const float *f, long long P, int pitch, int w,
 hipError_t launch_soa_to_aos(const float *f, float *aos, long long P, int pitch, int w, int h, hipStream_t s);
 hipError_t launch_halo_pack(const HaloArgs &a, hipStream_t s);
 hipError_t launch_halo_unpack(const HaloArgs &a, hipStream_t s);
-hipError_t resident_capacity(int variant, int device, int &capacity);
+hipError_t resident_capacity(int variant, int device, bool tol, int &capacity);
 int pipe_blocks(int w, int h);
 hipError_t launch_pipe_propagate(const float *f, float *t, long long P, int pitch, int w, int h, hipStream_t s);
 hipError_t launch_pipe_rebound(const float *t, float *f, const uint8_t *obst, long long P, int pitch, int w, int h,
@@ -66,7 +66,7 @@ hipError_t launch_pipe_rebound(const float *t, float *f, const uint8_t *obst, lo
 hipError_t launch_pipe_collision(const float *t, float *f, const uint8_t *obst, long long P, int pitch, int w, int h,
                                  float omega, float *partials, hipStream_t s);
 hipError_t launch_pipe_av(const float *partials, int n, float *av_local, int t, hipStream_t s);
-hipError_t launch_resident(const ResidentArgs &a, int variant, hipStream_t s);
+hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, hipStream_t s);
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s);
 }  // namespace lbm
 
@@ -986,7 +986,7 @@ struct lbm_handle {
             const int tx = (p.nx + RES_TWV[v] - 1) / RES_TWV[v];
             const int ty = (p.ny + RES_TH[v] - 1) / RES_TH[v];
             int cap = 0;
-            HIP_CHECK(resident_capacity(v, s.dev, cap));
+            HIP_CHECK(resident_capacity(v, s.dev, tolerance && RES_VER[v] == 2, cap));
             const long long n = (long long)tx * ty;
             if (n <= cap && n <= (long long)res_per_cu * cus) {
                 res_variant = v;
@@ -1047,6 +1047,9 @@ struct lbm_handle {
             a.omo = 1 - p.omega;
             a.w1 = p.density * p.accel / 9.f;
             a.w2 = p.density * p.accel / 36.f;
+            a.tc0 = p.omega * (4.f / 9.f);
+            a.tc1 = p.omega * (1.f / 9.f);
+            a.tc2 = p.omega * (1.f / 36.f);
             a.halo = res_halo;
             a.partials = res_partials;
             a.status = res_status;
@@ -1068,7 +1071,7 @@ struct lbm_handle {
                 HIP_CHECK(hipMemsetAsync(htrace, 0, n, s.s_comp));
                 a.htrace = htrace;
             }
-            HIP_CHECK(launch_resident(a, res_variant, s.s_comp));
+            HIP_CHECK(launch_resident(a, res_variant, tolerance && RES_VER[res_variant] == 2, s.s_comp));
             if (htrace) {  // per tile and step: wait for the slowest neighbour, then the hop itself
                 std::vector<unsigned long long> hv((size_t)2 * trace_steps * ntiles);
                 HIP_CHECK(hipMemcpyAsync(hv.data(), htrace, hv.size() * 8, hipMemcpyDeviceToHost, s.s_comp));
@@ -2064,7 +2067,9 @@ int lbm_placement_probe(lbm_handle *h, int32_t *kept, int32_t *tried, float *ms_
 
 int32_t lbm_numerics(lbm_handle *h) {
     if (!h) return -1;
-    return (h->tolerance && h->use_stream && h->fused && !h->resident && !h->pipeline) ? 1 : 0;
+    if (!h->tolerance || h->pipeline) return 0;
+    if (h->resident) return RES_VER[h->res_variant] == 2 ? 1 : 0;
+    return (h->use_stream && h->fused) ? 1 : 0;
 }
 
 const char *lbm_source_hash(void) { return LBM_SOURCE_HASH; }

@@ -204,6 +204,7 @@ struct ResidentArgs {
     unsigned tag0;          // granule tags of this run: tag0 + 1 .. tag0 + steps
     int accel_row;          // global row with the folded acceleration (-1: none)
     float omega, omo, w1, w2;
+    float tc0, tc1, tc2;    // LBM_FLAG_TOLERANCE collision: 4 omega / 9, omega / 9, omega / 36
     unsigned long long *halo;
     float *partials;        // [steps][ntiles]
     int *status;            // set to 1 when a neighbour hand-off timed out

@@ -313,7 +313,9 @@ __global__ __launch_bounds__(64 * NW) void resident_steps(ResidentArgs a) {
 // aligned): the unshifted pulls (N, S) are one ds_read_b64, the shifted ones
 // one ds_read2_b32, every write-back one ds_write_b64.
 // ---------------------------------------------------------------------------
-template <int NW, int TH, int MINW = 1>
+// TOL: the LBM_FLAG_TOLERANCE collision (collide2t, lbm_packed.hpp) instead
+// of the bitwise one -- same tiles, granules and schedule.
+template <int NW, int TH, int MINW = 1, bool TOL = false>
 __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a) {
     constexpr int NT = 64 * NW;
     constexpr int LS = RES2_TW + 4;
@@ -501,8 +503,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             const int lx = lxs[it], ly = lys[it];
             const float accf = (gy0 + ly == a.accel_row) ? 1.00f : 0.00f;
             f2 o[Q];
-            const f2 u = collide2(s[it], o, (oa >> it) & 1u, (ob >> it) & 1u, (anyo >> it) & 1u, accf, a.omega,
-                                  a.omo, a.w1, a.w2);
+            f2 u;
+            if constexpr (TOL) {
+                const bool oab = (oa >> it) & 1u, obb = (ob >> it) & 1u;
+                const f2 usq = collide2t(s[it], o, oab, obb, (anyo >> it) & 1u, accf != 0.00f,
+                                         TolK{a.omo, a.tc0, a.tc1, a.tc2}, a.w1, a.w2);
+                u = f2{oab ? 0.f : sqrt_av(usq.x), obb ? 0.f : sqrt_av(usq.y)};
+            } else {
+                u = collide2(s[it], o, (oa >> it) & 1u, (ob >> it) & 1u, (anyo >> it) & 1u, accf, a.omega, a.omo,
+                             a.w1, a.w2);
+            }
             tot += u.x + u.y;
             f0[it] = o[0];
 #pragma unroll
@@ -603,12 +613,15 @@ const void *resident_fn() {
 }
 
 template <int NW, int TH, int MINW = 1>
-const void *resident_fn2() {
-    return reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW>);
+const void *resident_fn2(bool tol) {
+    return tol ? reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW, true>)
+               : reinterpret_cast<const void *>(&resident_steps2<NW, TH, MINW, false>);
 }
 
 
-const void *resident_kernel(int variant, int &threads) {
+// tol selects the LBM_FLAG_TOLERANCE collision of the packed (v2) tiles; the
+// scalar v1 tiles have only the bitwise one
+const void *resident_kernel(int variant, int &threads, bool tol) {
     switch (variant) {
         case RES_64: threads = 1024; return resident_fn<16, 4>();
         case RES_32: threads = 1024; return resident_fn<16, 2>();
@@ -616,20 +629,20 @@ const void *resident_kernel(int variant, int &threads) {
         case RES_16x4: threads = 256; return resident_fn<4, 4>();
         case RES_8: threads = 512; return resident_fn<8, 1>();
         case RES_4: threads = 256; return resident_fn<4, 1>();
-        case RES2_32: threads = 1024; return resident_fn2<16, 32>();
-        case RES2_16: threads = 1024; return resident_fn2<16, 16>();
-        case RES2_16x8: threads = 512; return resident_fn2<8, 16, 4>();  // 2 blocks per CU: 4 waves per SIMD
-        case RES2_8: threads = 512; return resident_fn2<8, 8>();
-        case RES2_4: threads = 256; return resident_fn2<4, 4>();
-        default: threads = 128; return resident_fn2<2, 2>();  // RES2_2
+        case RES2_32: threads = 1024; return resident_fn2<16, 32>(tol);
+        case RES2_16: threads = 1024; return resident_fn2<16, 16>(tol);
+        case RES2_16x8: threads = 512; return resident_fn2<8, 16, 4>(tol);  // 2 blocks per CU: 4 waves per SIMD
+        case RES2_8: threads = 512; return resident_fn2<8, 8>(tol);
+        case RES2_4: threads = 256; return resident_fn2<4, 4>(tol);
+        default: threads = 128; return resident_fn2<2, 2>(tol);  // RES2_2
     }
 }
 }  // namespace
 
 // Blocks of `variant` the device keeps resident at once (occupancy query x CUs).
-hipError_t resident_capacity(int variant, int device, int &capacity) {
+hipError_t resident_capacity(int variant, int device, bool tol, int &capacity) {
     int threads = 0;
-    const void *fn = resident_kernel(variant, threads);
+    const void *fn = resident_kernel(variant, threads, tol);
     int per_cu = 0, cus = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0);
     if (e != hipSuccess) return e;
@@ -639,9 +652,9 @@ hipError_t resident_capacity(int variant, int device, int &capacity) {
     return hipSuccess;
 }
 
-hipError_t launch_resident(const ResidentArgs &a, int variant, hipStream_t s) {
+hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, hipStream_t s) {
     int threads = 0;
-    const void *fn = resident_kernel(variant, threads);
+    const void *fn = resident_kernel(variant, threads, tol);
     ResidentArgs arg = a;
     void *params[] = {&arg};
     // cooperative: the runtime rejects a grid that cannot be fully resident

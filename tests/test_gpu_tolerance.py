@@ -35,17 +35,23 @@ def _rel(a, b):
     return float(np.max(np.abs(a.astype(np.float64) - b) / np.maximum(np.abs(b.astype(np.float64)), 1e-30)))
 
 
+@pytest.mark.parametrize("kernel", ["stream", "resident"])
 @pytest.mark.parametrize("grid", GRIDS)
-def test_tolerance_reference_grids_check_py(gpu_lib, grid, tmp_path):
+def test_tolerance_reference_grids_check_py(gpu_lib, grid, kernel, tmp_path):
+    """Full maxIters with the tolerance collision (stream kernel, and the packed
+    resident tiles AUTO picks for these grids): check.py passes, av_vels close
+    to the oracle's."""
     p, obst = load_problem(grid)
-    with gpu_lib.Engine(p, obst, **_tol_kw(gpu_lib)) as e:
-        assert e.kernel_in_use() == "stream" and e.numerics() == "tolerance"
+    kw = dict(kernel=gpu_lib.KERNEL_STREAM if kernel == "stream" else gpu_lib.KERNEL_RESIDENT,
+              flags=gpu_lib.FLAG_TOLERANCE)
+    with gpu_lib.Engine(p, obst, **kw) as e:
+        assert e.kernel_in_use() == kernel and e.numerics() == "tolerance"
         e.load_cells(lio.init_cells(p))
         e.run()
         cells, av = e.store()
     assert np.isfinite(cells).all()
     dev = float(np.max(np.abs(av - oracle_av_vels(grid)) / np.abs(oracle_av_vels(grid))))
-    print(f"{grid}: av_vels max relative deviation from the oracle {dev:.3e}")
+    print(f"{grid} {kernel}: av_vels max relative deviation from the oracle {dev:.3e}")
     assert dev < TOL_AV * 10
     lio.write_average_velocities(str(tmp_path / "av_vels.dat"), av)
     ref_av = lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz")
@@ -102,16 +108,39 @@ def test_tolerance_decomposition_invariant(gpu_lib):
 
 
 def test_tolerance_flag_keeps_other_kernels_bitwise(gpu_lib):
-    """The flag changes only the fused stream launches: step2 / resident / vec4
-    handles report bitwise numerics and stay equal to the oracle."""
+    """The flag changes only the fused stream launches and the packed resident
+    tiles: step2 / vec4 handles report bitwise numerics and stay equal to the
+    oracle."""
     p, obst = load_problem("128x128", iters=50)
     cells0 = lio.init_cells(p)
     ref, _ = oracle.run(p, obst, 50, cells0)
-    for kernel, extra in ((gpu_lib.KERNEL_STEP2, 0), (gpu_lib.KERNEL_RESIDENT, 0),
-                          (gpu_lib.KERNEL_VEC4, gpu_lib.FLAG_ONE_STEP)):
+    for kernel, extra in ((gpu_lib.KERNEL_STEP2, 0), (gpu_lib.KERNEL_VEC4, gpu_lib.FLAG_ONE_STEP)):
         with gpu_lib.Engine(p, obst, kernel=kernel, flags=gpu_lib.FLAG_TOLERANCE | extra) as e:
             assert e.numerics() == "bitwise"
             e.load_cells(cells0)
             e.run_steps(50, accelerate_first=True)
             cells, _ = e.store(n_av=50)
         assert np.array_equal(cells, ref)
+
+
+@pytest.mark.parametrize("th", [4, 8, 16])
+def test_tolerance_resident_tiles_vs_stream(gpu_lib, th, monkeypatch):
+    """The resident tiles' tolerance collision is the stream kernel's
+    (collide2t): the same lattice bit for bit on a problem both run."""
+    monkeypatch.setenv("LBM_RES_TH", str(th))
+    monkeypatch.setenv("LBM_RES_V", "2")
+    rng = np.random.default_rng(th)
+    p = lio.Params(256, 96, 18, 10, 0.1, 0.02, 1.7)  # 18: whole 6-step stream launches
+    obst = (rng.random((96, 256)) < 0.03).astype(np.uint8)
+    obst[0, :] = 1
+    cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((96, 256, 9)))).astype(np.float32)
+    out = {}
+    for kernel in (gpu_lib.KERNEL_RESIDENT, gpu_lib.KERNEL_STREAM):
+        with gpu_lib.Engine(p, obst, kernel=kernel, flags=gpu_lib.FLAG_TOLERANCE, steps_per_launch=0) as e:
+            assert e.numerics() == "tolerance"
+            e.load_cells(cells0)
+            e.run_steps(18, accelerate_first=True)
+            out[kernel] = e.store(n_av=18)
+    a, b = out[gpu_lib.KERNEL_RESIDENT], out[gpu_lib.KERNEL_STREAM]
+    assert np.array_equal(a[0], b[0])
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-5)
