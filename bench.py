@@ -287,7 +287,7 @@ def _agree_max(v: int, dist_on: bool) -> int:
     return int(t[0])
 
 
-def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_on: bool) -> dict:
+def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_on: bool, flags: int = 0) -> dict:
     """BASELINE config 5: D3Q19 n^3 channel (body force between wall planes y = 0 and
     y = n-1), z slabs over all ranks (RCCL: two ghost planes each way per
     two-step pass, overlapped with the slab interior), whole-job MLUPS (strong
@@ -297,7 +297,7 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
     import torch.distributed as dist
     p = lio.Params3D(n, n, n, steps, 0.1, 0.001, 1.85)
     obst = lio.channel_obstacles3d(n, n, n)
-    kw = dict(devices=[local_rank])
+    kw = dict(devices=[local_rank], flags=flags)
     if dist_on:
         box = [native.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
@@ -329,6 +329,7 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
     alg_b = 19 * 4 * (768 / 480 + 1) / 2 if two else 152
     per_gpu_gbs = alg_b * cells / world * steps / dev / 1e9
     return {"grid": f"{n}^3", "steps": steps, "settle_steps": nset, "decomposition": f"{world} z slabs",
+            "numerics": "tolerance" if flags & native.FLAG_TOLERANCE else "bitwise",
             "kernel": "step3d_two (2 steps per pass)" if two else "step3d_pair (1 step per launch)",
             "mlups": round(cells * steps / secs / 1e6, 1), "ms_per_step": round(secs / steps * 1e3, 4),
             "hbm_gbs_per_gpu": round(per_gpu_gbs, 1), "hbm_frac": round(per_gpu_gbs / HBM_PEAK_GBS, 4),
@@ -646,6 +647,11 @@ def main() -> int:
             aux["config5_d3q19"] = aux_d3q19(args.d3q19_n, 20, rank, world, local_rank, dist_on)
         except Exception as exc:
             aux["config5_d3q19"] = {"error": str(exc)}
+        try:
+            aux["config5_d3q19_tolerance"] = aux_d3q19(args.d3q19_n, 20, rank, world, local_rank, dist_on,
+                                                       flags=native.FLAG_TOLERANCE)
+        except Exception as exc:
+            aux["config5_d3q19_tolerance"] = {"error": str(exc)}
     if rank == 0 and n == 1:
         if not args.no_aux:
             try:

@@ -38,7 +38,10 @@
  *
  * Placement reuses lbm_config (lbm_hip.h): parts = z slabs, transport LOCAL
  * (all slabs in this process, device copies) or RCCL (one slab per rank);
- * kernel / graph / flags fields are ignored.
+ * kernel / graph fields are ignored; flags may carry LBM_FLAG_TOLERANCE: the
+ * two-step passes then use the reciprocal collision (one v_rcp_f32 + Newton
+ * step for u, FMA contraction; not bitwise equal to the restatement, within
+ * the tolerance tests/test_d3q19.py states), one-step launches stay bitwise.
  */
 #ifndef LBM3D_HIP_H
 #define LBM3D_HIP_H

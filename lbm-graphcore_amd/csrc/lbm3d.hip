@@ -221,6 +221,71 @@ __device__ __forceinline__ float cell3d(const float (&s)[Q3], float (&o)[Q3], bo
     return __builtin_amdgcn_sqrtf(usq);  // |u| feeds av_vels only (<= 1 ulp, as lbm_packed.hpp sqrt_av)
 }
 
+// LBM_FLAG_TOLERANCE form of cell3d (the 2-D collide2t's reassociation in
+// 3-D): one reciprocal of rho (v_rcp_f32 + a Newton step) for u_x, u_y, u_z,
+// rho * (omega / 3 | 18 | 36), out_k = fma(s_k, 1 - omega, P +- Q) per pair of
+// opposite speeds with P = ld (4.5 v^2 + c), Q = 3 ld v.  Not bitwise equal to
+// oracle/lbm_oracle3d.c; checked against it within a stated tolerance
+// (tests/test_d3q19.py test_d3q19_tolerance_*).  k = {1 - omega, omega/3,
+// omega/18, omega/36}.
+__device__ __forceinline__ float cell3dt(const float (&s)[Q3], float (&o)[Q3], bool ob, float omo, float k0, float k1,
+                                         float k2, float w1, float w2) {
+    if (ob) {
+        o[0] = s[0];
+        o[1] = s[2];
+        o[2] = s[1];
+        o[3] = s[4];
+        o[4] = s[3];
+        o[5] = s[6];
+        o[6] = s[5];
+        o[7] = s[8];
+        o[8] = s[7];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            o[9 + i] = s[14 + i];
+            o[14 + i] = s[9 + i];
+        }
+        return 0.f;
+    }
+    const float ax = s[1] + s[5] + s[7] + s[10] + s[16], bx = s[2] + s[6] + s[8] + s[11] + s[15];
+    const float ay = s[3] + s[5] + s[8] + s[12] + s[18], by = s[4] + s[6] + s[7] + s[13] + s[17];
+    const float az = s[9] + s[10] + s[11] + s[12] + s[13], bz = s[14] + s[15] + s[16] + s[17] + s[18];
+    const float rho = ((s[0] + (s[3] + s[4])) + (ax + bx)) + (az + bz);
+    float r = __builtin_amdgcn_rcpf(rho);
+    r = __builtin_fmaf(r, __builtin_fmaf(-rho, r, 1.00f), r);
+    const float ux = (ax - bx) * r, uy = (ay - by) * r, uz = (az - bz) * r;
+    const float usq = __builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz));
+    const float c = __builtin_fmaf(usq, -1.50f, 1.00f);
+    const float ld1 = rho * k1, ld2 = rho * k2;
+    const float l3 = ld1 * 3.00f, m3 = ld2 * 3.00f;
+    o[0] = __builtin_fmaf(s[0], omo, (rho * k0) * c);
+    auto pair = [&](int kp, int km, float v, float ld, float ld3) {
+        const float p = ld * __builtin_fmaf(v * v, 4.50f, c), q = ld3 * v;
+        o[kp] = __builtin_fmaf(s[kp], omo, p + q);
+        o[km] = __builtin_fmaf(s[km], omo, p - q);
+    };
+    pair(1, 2, ux, ld1, l3);
+    pair(3, 4, uy, ld1, l3);
+    pair(9, 14, uz, ld1, l3);
+    pair(5, 6, ux + uy, ld2, m3);
+    pair(7, 8, ux - uy, ld2, m3);
+    pair(10, 15, ux + uz, ld2, m3);
+    pair(11, 16, uz - ux, ld2, m3);
+    pair(12, 17, uy + uz, ld2, m3);
+    pair(13, 18, uz - uy, ld2, m3);
+    o[1] = o[1] + w1;
+    o[2] = o[2] - w1;
+    o[5] = o[5] + w2;
+    o[6] = o[6] - w2;
+    o[7] = o[7] + w2;
+    o[8] = o[8] - w2;
+    o[10] = o[10] + w2;
+    o[11] = o[11] - w2;
+    o[15] = o[15] - w2;
+    o[16] = o[16] + w2;
+    return __builtin_amdgcn_sqrtf(usq);
+}
+
 // Two cells per lane (a column pair, nx even): every load and store is a
 // float2 (512 B per wave instruction instead of 256); the x-shifted pulls
 // take the neighbour column from the adjacent lane by DPP, and the first /
@@ -367,6 +432,7 @@ struct Two3Args {
     int px, nx, ny, nz, seg;
     int z0, zn;           // output planes [z0, zn) of this launch, in segments of seg planes
     float omega, omo, w1, w2;
+    float k0, k1, k2;     // tolerance collision: omega / 3, omega / 18, omega / 36
     float *partials;      // [2][nblocks]: |u| of step t+1, then t+2, at blk0 + this launch's block
     int nblocks, blk0;
 };
@@ -374,7 +440,7 @@ struct Two3Args {
 // One level for centre plane jz - 1, input plane jz (in).  Must be reached by
 // every thread of the block (it holds a barrier).  live (wave-uniform): some
 // later level or output needs this row's result.
-template <int TH>
+template <int TH, bool TOL>
 __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3], float *lds, int jz, float (&r0)[3],
                                         float (&r9a)[3], float (&r9b)[3], int lane, int wy, bool ob, bool live,
                                         const Two3Args &a) {
@@ -415,7 +481,10 @@ __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3],
     s[18] = M[T3C + wm + lane];
     float u = 0.f;
     if (live) {
-        u = cell3d(s, out, ob, a.omega, a.omo, a.w1, a.w2);
+        if constexpr (TOL)
+            u = cell3dt(s, out, ob, a.omo, a.k0, a.k1, a.k2, a.w1, a.w2);
+        else
+            u = cell3d(s, out, ob, a.omega, a.omo, a.w1, a.w2);
     } else {
 #pragma unroll
         for (int k = 0; k < Q3; ++k) out[k] = 0.f;
@@ -431,7 +500,7 @@ __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3],
 
 // PD: input planes in flight -- 1: plane j+1 while j is computed; 2: also j+2
 // (19 more VGPRs; one 768..960-thread block per CU keeps few loads in flight).
-template <int TH, bool SKIP, int PD>
+template <int TH, bool SKIP, int PD, bool TOL = false>
 __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
     __shared__ float lds1[T3<TH>::LDS], lds2[T3<TH>::LDS];
     __shared__ float red[2][TH];
@@ -480,9 +549,9 @@ __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
         ob2 = ob1;
         ob1 = obz(j - 1);
         float o1[Q3], o2[Q3];
-        const float v1 = level3<TH>(in, o1, lds1, j, r0a, r9aa, r9ba, lane, wy, ob1, live1, a);
+        const float v1 = level3<TH, TOL>(in, o1, lds1, j, r0a, r9aa, r9ba, lane, wy, ob1, live1, a);
         if (own && j - 1 >= zs && j - 1 < ze) u1 += v1;
-        const float v2 = level3<TH>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, lane, wy, ob2, live2, a);
+        const float v2 = level3<TH, TOL>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, lane, wy, ob2, live2, a);
         if (own && j - 2 >= zs && j - 2 < ze) {
             u2 += v2;
             float *d = a.fout + (long long)(j - 2) * a.PL + row;
@@ -620,6 +689,7 @@ struct lbm3d_handle {
     long long kspad = 0;  // LBM3D_KSPAD: floats appended to each speed plane (multiple of 64)
     const char *lattice_pad = nullptr;  // LBM_LATTICE_PAD (debug knob)
     bool poison = false;  // LBM_POISON=1: fresh allocations filled with NaN bytes
+    bool tolerance = false;  // LBM_FLAG_TOLERANCE: the two-step passes use cell3dt (not bitwise)
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
     ncclComm_t comm = nullptr;
@@ -643,6 +713,7 @@ struct lbm3d_handle {
         if (!obstacles) throw fail3(LBM_E_INVALID, "obstacles must not be NULL");
         parts = cfg.parts > 0 ? cfg.parts : 1;
         transport = cfg.transport;
+        tolerance = (cfg.flags & LBM_FLAG_TOLERANCE) != 0;
         if (parts > p.nz) throw fail3(LBM_E_INVALID, "more z slabs than planes");
         int ndev = 0;
         H3(hipGetDeviceCount(&ndev));
@@ -671,6 +742,11 @@ struct lbm3d_handle {
         if (const char *d = knob("LBM3D_PD")) pd = atoi(d);
         if (const char *k = knob("LBM3D_KSPAD")) kspad = (std::max(0LL, atoll(k)) + 63) / 64 * 64;
         lattice_pad = knob("LBM_LATTICE_PAD");
+        if (tolerance) {  // the tolerance pass exists for the default block only
+            th = 12;
+            skip = false;
+            pd = 1;
+        }
         // the two-step kernel is instantiated for these (rows, skip, prefetch)
         // combinations only; anything else is rejected here, never launched as
         // a different template (blocks of 64 x th threads, at most 960)
@@ -850,11 +926,19 @@ struct lbm3d_handle {
         a.omo = 1 - p.omega;
         a.w1 = w1();
         a.w2 = w2();
+        a.k0 = p.omega * (1.f / 3.f);
+        a.k1 = p.omega * (1.f / 18.f);
+        a.k2 = p.omega * (1.f / 36.f);
         a.partials = s.partials2;
         a.nblocks = s.nblk_two;
         a.blk0 = blk0;
         const dim3 g((p.nx + T3OX - 1) / T3OX, (p.ny + th - 5) / (th - 4), (zn - z0 + seg - 1) / seg);
         const dim3 b(T3W, th);
+        if (tolerance) {  // the default block only (12 rows, no skip, one plane prefetched)
+            hipLaunchKernelGGL((step3d_two<12, false, 1, true>), g, b, 0, st, a);
+            H3(hipGetLastError());
+            return;
+        }
         switch (two_variant(th, skip, pd)) {
             case 48: hipLaunchKernelGGL((step3d_two<12, false, 1>), g, b, 0, st, a); break;
             case 49: hipLaunchKernelGGL((step3d_two<12, false, 2>), g, b, 0, st, a); break;

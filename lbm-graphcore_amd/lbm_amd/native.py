@@ -367,7 +367,7 @@ class Engine3D:
     """One lbm3d_handle: the D3Q19 extension engine (include/lbm3d_hip.h)."""
 
     def __init__(self, params, obstacles: np.ndarray, *, parts: int = 1, transport: int = TRANSPORT_LOCAL,
-                 rank: int = 0, world: int = 1, devices=None, unique_id: bytes | None = None):
+                 rank: int = 0, world: int = 1, devices=None, unique_id: bytes | None = None, flags: int = 0):
         self._L = load_library()
         self.params = Params3D(int(params.nx), int(params.ny), int(params.nz), int(params.max_iters),
                                float(params.density), float(params.accel), float(params.omega))
@@ -377,6 +377,7 @@ class Engine3D:
         cfg = Config()
         cfg.parts = int(world if transport == TRANSPORT_RCCL else parts)
         cfg.transport = transport
+        cfg.flags = int(flags)  # FLAG_TOLERANCE: the two-step passes use the reciprocal collision
         cfg.rank, cfg.world = int(rank), int(world)
         if devices:
             self._devs = (ctypes.c_int32 * len(devices))(*devices)

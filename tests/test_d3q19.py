@@ -276,3 +276,21 @@ def test_d3q19_lattice_placement_bitwise(gpu_lib, nx, ny, nz, parts, two, env, m
     bad = np.argwhere(cells != ref)
     assert len(bad) == 0, (len(bad), bad[:8].tolist(), sorted(set(bad[:, 0].tolist())), sorted(set(bad[:, 3].tolist())))
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [1, 3])
+def test_d3q19_tolerance_vs_oracle(gpu_lib, parts):
+    """LBM_FLAG_TOLERANCE (cell3dt in the two-step passes): every population
+    within 2e-5 relative of the restatement after 8 steps (four two-step
+    passes), av_vels within 1e-4, and the tolerance result does not depend on
+    the slab decomposition (bitwise equal to one slab)."""
+    p, obst, c0 = _problem(70, 31, 24, 99)
+    ref, ref_av = oracle.run3d(p, obst, 8, c0)
+    one, _ = _gpu3d(gpu_lib, p, obst, c0, 8, devices=[0], flags=gpu_lib.FLAG_TOLERANCE)
+    cells, av = _gpu3d(gpu_lib, p, obst, c0, 8, parts=parts, devices=[0], flags=gpu_lib.FLAG_TOLERANCE)
+    dev = float(np.max(np.abs(cells.astype(np.float64) - ref) / np.maximum(np.abs(ref), 1e-30)))
+    assert dev < 2e-5, dev
+    assert not np.array_equal(cells, ref)  # the flag really selects the other collision
+    assert np.array_equal(cells, one)
+    np.testing.assert_allclose(av, ref_av, rtol=1e-4)
