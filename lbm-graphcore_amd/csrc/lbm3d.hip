@@ -250,7 +250,8 @@ __device__ __forceinline__ float cell3dt(const float (&s)[Q3], float (&o)[Q3], b
     const float ax = s[1] + s[5] + s[7] + s[10] + s[16], bx = s[2] + s[6] + s[8] + s[11] + s[15];
     const float ay = s[3] + s[5] + s[8] + s[12] + s[18], by = s[4] + s[6] + s[7] + s[13] + s[17];
     const float az = s[9] + s[10] + s[11] + s[12] + s[13], bz = s[14] + s[15] + s[16] + s[17] + s[18];
-    const float rho = ((s[0] + (s[3] + s[4])) + (ax + bx)) + (az + bz);
+    // ax + bx holds speeds 1, 2, 5-8, 10, 11, 15, 16; the rest of the 19 here
+    const float rho = ((s[0] + (s[3] + s[4])) + (ax + bx)) + ((s[9] + s[12] + s[13]) + (s[14] + s[17] + s[18]));
     float r = __builtin_amdgcn_rcpf(rho);
     r = __builtin_fmaf(r, __builtin_fmaf(-rho, r, 1.00f), r);
     const float ux = (ax - bx) * r, uy = (ay - by) * r, uz = (az - bz) * r;
