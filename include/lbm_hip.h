@@ -56,8 +56,10 @@ typedef struct lbm_params {
 enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
 /* Step kernels.  SCALAR / VEC4: one time step per launch (VEC4 needs widths
  * that are multiples of 4).  STEP2: fused two-step launches through LDS.
- * STREAM: fused S-step launches (S = steps_per_launch, 2..6; default 6) streaming rows
- * through registers.  RESIDENT: every step of a run in one persistent
+ * STREAM: fused S-step launches (S = steps_per_launch, 2..6, 2..8 with
+ * LBM_FLAG_TOLERANCE; default 6) streaming rows through registers; a run of
+ * K steps on one sub-domain is K / S launches plus, when 2 <= K % S, one
+ * fused launch of K % S steps (else K % S one-step launches).  RESIDENT: every step of a run in one persistent
  * launch with the lattice held on chip (LDS + registers) -- single
  * sub-domain grids small enough for all of their 64-column tiles to be
  * co-resident (1024x1024 and below on MI355X).  PIPELINE: the unfused
@@ -106,7 +108,8 @@ typedef struct lbm_config {
     int32_t graph_steps;    /* >0: replay the step loop as hipGraphs of 2*graph_steps steps
                                (single sub-domain without exchange); <0: off; 0: library default */
     int32_t flags;          /* LBM_FLAG_* */
-    int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..6); 0 = library default (6) */
+    int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..6; 2..8 with LBM_FLAG_TOLERANCE);
+                                 0 = library default (6) */
 } lbm_config;
 
 /* Route the periodic wrap of undecomposed dimensions through the transport
@@ -121,11 +124,11 @@ typedef struct lbm_config {
  * correctly rounded divisions, the constant divisions by 9 and 36 folded into
  * multiplications, and FMA contraction.  Still IEEE fp32 arithmetic, but no
  * longer bitwise equal to LastChance.cpp:226-262: after 100 steps at 8192^2
- * every population stays within 2e-6 relative of the oracle, and check.py
+ * every population stays within 2e-5 relative of the oracle, and check.py
  * passes on all four reference grids (tests/test_gpu_tolerance.py).  The
- * packed RESIDENT tiles take the same collision; the other kernels
- * (remainder one-step launches, STEP2, VEC4, the scalar resident tiles) stay
- * bitwise.
+ * packed RESIDENT tiles take the same collision (and the D3Q19 engine's
+ * two-step passes); the other kernels (one-step remainder launches, STEP2,
+ * VEC4, the scalar resident tiles) stay bitwise.
  * lbm_numerics() reports which mode a handle runs. */
 #define LBM_FLAG_TOLERANCE 4
 

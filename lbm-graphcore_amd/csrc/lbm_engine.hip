@@ -46,6 +46,7 @@ hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hi
 hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t s);
 hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s);
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n);
+bool s2d_form_ok(int steps, int cfg, bool tol);
 hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, hipStream_t s);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
@@ -294,7 +295,7 @@ struct lbm_handle {
         auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
         stream_cfg = form(knob("LBM_STREAM_CFG", stream_cfg), stream_cfg);
         tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
-        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 6);
+        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 8);
         stream_min_cells = std::max(0, knob("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         {
             const char *g = knob_str("LBM_STREAM_GUIDE");
@@ -539,6 +540,7 @@ struct lbm_handle {
         b3.w = s.w;
         b3.h = s.h;
         b3.xmax = s.rf - xoff - 1;  // last column inside the row allocation (>= w + gr + 1)
+        b3.hw = hw;
         b3.gy0 = s.rect.y0;
         b3.ny = p.ny;
         b3.accel_g = p.ny >= 2 ? p.ny - 2 : -1;
@@ -854,13 +856,16 @@ struct lbm_handle {
         // every sub-domain at least S cells (2S across a decomposed dimension)
         // launch form: the tolerance collision has forms 0 and 4 only
         if (tolerance) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
-        // the v3 kernel takes up to 6 steps per launch (8 in the LP form)
-        const int s_max = 6;
+        // the v3 kernel takes up to 6 steps per launch, 8 in the tolerance LP form
+        const int s_max = tolerance ? 8 : 6;
         const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch
                                                : std::min(tolerance ? tol_s : stream_s, s_max);
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
-            throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max));
-        if (stream_cfg == 4 && S != 6) stream_cfg = 0;  // the LP form exists for S = 6 (below it: no gain)
+            throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max) +
+                                                 (tolerance ? "" : " (up to 8 with LBM_FLAG_TOLERANCE)"));
+        // the LP form exists for S = 6 (bitwise) and 6..8 (tolerance); S = 7, 8 have only it
+        if (S > 6) stream_cfg = 4;
+        if (!s2d_form_ok(S, stream_cfg, tolerance)) stream_cfg = 0;
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;
@@ -1504,11 +1509,16 @@ struct lbm_handle {
 
     // Interior (reducing) or boundary launch of sub-domain s reading parity
     // `cur`: one fused launch (spl steps, WG halo) or one step (W1 halo).
-    hipError_t launch_part(Sub &s, int cur, bool fused_launch, bool interior, hipStream_t st) const {
+    // steps > 0 (single sub-domain stream engines): a remainder launch of that
+    // many fused steps (< spl) on the same work split and halo tables.
+    hipError_t launch_part(Sub &s, int cur, bool fused_launch, bool interior, hipStream_t st, int steps = 0) const {
         if (fused_launch && use_stream) {
             const int n = interior ? s.n3_int : s.n3_bnd;
             if (n <= 0) return hipSuccess;
             const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
+            if (steps > 0 && steps != spl)
+                return launch_stream2d(a, n, steps, interior, s2d_form_ok(steps, stream_cfg, tolerance) ? stream_cfg : 0,
+                                       tolerance, st);
             return launch_stream2d(a, n, spl, interior, stream_cfg, tolerance, st);
         }
         if (fused_launch) {
@@ -1531,10 +1541,11 @@ struct lbm_handle {
     //        never read the ghost ring, so the exchange of launch t-1 runs
     //        under I(t) and B(t+1) overlaps I(t+1)'s tail.
     // join() re-serialises everything onto s_comp.
-    void launch_once(bool two) {
+    // steps > 0: a fused remainder launch of that many steps (< spl).
+    void launch_once(bool two, int steps = 0) {
         if (!multi()) {
             Sub &s = subs[0];
-            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp));
+            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp, steps));
             s.cur ^= 1;
             return;
         }
@@ -1551,7 +1562,7 @@ struct lbm_handle {
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
             wait_exchange_on(s, s.s_bnd);
-            HIP_CHECK(launch_part(s, s.cur, two, false, s.s_bnd));
+            HIP_CHECK(launch_part(s, s.cur, two, false, s.s_bnd, steps));
             HIP_CHECK(hipEventRecord(s.ev_b, s.s_bnd));
             HIP_CHECK(hipEventRecord(s.ev_bp[s.cur], s.s_bnd));
             tgt[k] = s.o[1 - s.cur];
@@ -1560,7 +1571,7 @@ struct lbm_handle {
         for (auto &s : subs) {
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_comp, s.ev_bp[1 - s.cur], 0));  // B(t-1)
-            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp));
+            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp, steps));
             HIP_CHECK(hipEventRecord(s.ev_i, s.s_comp));
         }
         for (auto &s : subs) s.cur ^= 1;
@@ -1667,10 +1678,20 @@ struct lbm_handle {
             for (; l + chunk <= launches; l += chunk) HIP_CHECK(hipGraphLaunch(ge, s0.s_comp));
         }
         for (; l < launches; ++l) launch_once(fused);
-        const int rem = steps - launches * per_launch;
-        for (int i = 0; i < rem; ++i) launch_once(false);  // remainder: one-step kernel (W1 halo) ...
-        run_fused = fused ? launches : 0;
-        run_single = fused ? rem : launches;
+        int rem = steps - launches * per_launch;
+        // remainder of a stream engine (2 <= rem < spl): ONE fused launch of
+        // rem steps on the same work split and boundary bands (the strips'
+        // overlap and the ghost ring are sized for spl >= rem).  The halo
+        // tables and send buffers are laid out for spl; halo_out_g puts a
+        // shorter launch's halo cells in the innermost rem ghost columns / rows
+        // (send-buffer positions), where the periodic / neighbour images of
+        // its cells belong, so the exchange of this launch leaves the rem-deep
+        // ring right and refresh_halos below restores the whole spl-deep ring
+        const bool fused_rem = fused && use_stream && rem >= 2;
+        if (fused_rem) launch_once(true, rem);
+        for (int i = 0; i < (fused_rem ? 0 : rem); ++i) launch_once(false);  // remainder: one-step kernel (W1 halo) ...
+        run_fused = fused ? launches + (fused_rem ? 1 : 0) : 0;
+        run_single = fused ? (fused_rem ? 0 : rem) : launches;
         join();
         if (rem > 0) refresh_halos();                      // ... then restore the WG ring for the next launch
         for (auto &s : subs) {

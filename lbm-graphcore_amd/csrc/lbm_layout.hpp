@@ -154,6 +154,7 @@ struct StreamArgs {
     long long plane;
     int pitch, ogp, og;
     int w, h, xmax;         // xmax: last column inside the row allocation (>= w + gr + 1)
+    int hw;                 // WG halo width of the dst tables (the engine's steps per launch; >= S of any launch)
     int gy0, ny, accel_g;
     float omega, omo, w1, w2;
     float tc0, tc1, tc2;    // LBM_FLAG_TOLERANCE collision: 4 omega / 9, omega / 9, omega / 36

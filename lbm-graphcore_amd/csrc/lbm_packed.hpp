@@ -227,6 +227,10 @@ __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
         cc[8] = fma2(s[8], omo, p - q);
     }
     if (accrow) {
+        // a real (wave-uniform) branch: without this barrier to speculation
+        // the compiler if-converts it into 6 adds + 12 selects on EVERY row
+        // (and holds their results in registers)
+        asm volatile("" ::: "memory");
         const f2 a1 = mk2(w1), a2 = mk2(w2);
         cc[1] = cc[1] + a1;
         cc[3] = cc[3] - a1;

@@ -36,8 +36,14 @@ __device__ __forceinline__ Dst2 ld_dst(CDst2 *p) {
     return d;
 }
 
+// S: the launch's steps (cells x < S or >= w - S are halo cells); the tables
+// are laid out for the engine's ring width a.hw >= S, so east / north
+// positions count from w - hw (h - hw): a remainder launch of fewer steps
+// writes the innermost S of the hw ghost columns (rows), where the periodic /
+// neighbour images of its cells belong.
 __device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, int y, const float (&o)[Q]) {
     const bool east = x >= a.w - S, west = x < S, north = y >= a.h - S, south = y < S;
+    const int ex = x - (a.w - a.hw), ny = y - (a.h - a.hw);
     // The table is launch-invariant: read through the constant address space
     // under wave-uniform branches it becomes scalar loads, which never make
     // the wave wait for its row prefetch (a vector load here would need a
@@ -46,7 +52,7 @@ __device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, in
     const bool any_e = __builtin_amdgcn_ballot_w64(east) != 0, any_w = __builtin_amdgcn_ballot_w64(west) != 0;
     if (any_e) {
         const Dst2 d = ld_dst(dg + DE);
-        if (east) store2(d, x - (a.w - S), y, o);
+        if (east) store2(d, ex, y, o);
     }
     if (any_w) {
         const Dst2 d = ld_dst(dg + DW);
@@ -54,14 +60,14 @@ __device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, in
     }
     if (north) {
         const Dst2 d = ld_dst(dg + DN);
-        store2(d, y - (a.h - S), x, o);
+        store2(d, ny, x, o);
         if (any_e) {
             const Dst2 e = ld_dst(dg + DNE);
-            if (east) store2(e, y - (a.h - S), x - (a.w - S), o);
+            if (east) store2(e, ny, ex, o);
         }
         if (any_w) {
             const Dst2 w = ld_dst(dg + DNW);
-            if (west) store2(w, y - (a.h - S), x, o);
+            if (west) store2(w, ny, x, o);
         }
     }
     if (south) {
@@ -73,7 +79,7 @@ __device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, in
         }
         if (any_e) {
             const Dst2 e = ld_dst(dg + DSE);
-            if (east) store2(e, y, x - (a.w - S), o);
+            if (east) store2(e, y, ex, o);
         }
     }
 }
@@ -139,7 +145,9 @@ __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2
 // instead of registers -- lpl points at this lane's slot of a per-wave
 // [S][3][64] f2 array; each level reads row y-1 from it and writes row y
 // back (the same lane, the same address: no barrier, LDS keeps a wave's
-// order) -- 6 VGPRs fewer per level, so S = 6..8 fit without spills.
+// order) -- 6 VGPRs fewer per level -- and the per-level |u| sums follow it
+// ([S][64], .x): S VGPRs fewer.  Tolerance forms fit S = 8 at two waves per
+// SIMD, the bitwise form S = 6.
 template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL, bool LP>
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j,
                                              const TolK &tk, f2 *lpl) {
@@ -220,7 +228,10 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         if (rowlive) {
             const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
             const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
-            st.tot[b] += ua + ub;
+            if constexpr (LP)
+                lpl[(3 * S + b) * 64].x += ua + ub;  // LP: the per-level |u| sums in LDS, not VGPRs
+            else
+                st.tot[b] += ua + ub;
         }
         if (L == S) {
             if (rowlive && (g.owna || g.ownb)) {
@@ -355,13 +366,18 @@ __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, 
 template <int S, bool kReduce, int W, bool NT, bool TOL = false, bool LP = false>
 __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     __shared__ float lds[W];
-    __shared__ f2 lds_p[LP ? W * 3 * S * 64 : 1];  // LP: [wave][S][3][64]
+    __shared__ f2 lds_p[LP ? W * 4 * S * 64 : 1];  // LP: [wave] {[S][3][64] rows, [S][64] |u| sums}
     if (kReduce && blockIdx.x == 0) reduce_pending_n<64 * W>(a.ctl, a.partials_prev, a.av_local, lds);
 
     const int lane = threadIdx.x & 63;
     Stream2State<S> st;
 #pragma unroll
     for (int l = 0; l < S; ++l) st.tot[l] = 0.f;
+    f2 *const lpl = lds_p + (LP ? (threadIdx.x >> 6) * 4 * S * 64 : 0) + lane;
+    if constexpr (LP) {
+#pragma unroll
+        for (int l = 0; l < S; ++l) lpl[(3 * S + l) * 64] = mk2(0.f);
+    }
     // wave-uniform: keeps the unit geometry and the row loop in scalar registers
     const int slot = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6));
     // dispatch order -> work unit (a.uperm: per XCD range, obstacle-bearing
@@ -375,9 +391,13 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
         // read no obstacle cell run the select-free copy of the unit loop
         typedef const __attribute__((address_space(4))) uint8_t CU8;
         if (a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0)
-            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lds_p + (LP ? (threadIdx.x >> 6) * 3 * S * 64 : 0) + lane);
+            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lpl);
         else
-            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lds_p + (LP ? (threadIdx.x >> 6) * 3 * S * 64 : 0) + lane);
+            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lpl);
+    }
+    if constexpr (LP) {
+#pragma unroll
+        for (int l = 0; l < S; ++l) st.tot[l] = lpl[(3 * S + l) * 64].x;
     }
     if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
@@ -413,6 +433,8 @@ hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, h
         case 4: hipLaunchKernelGGL(stream2d_flags<4>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 5: hipLaunchKernelGGL(stream2d_flags<5>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 6: hipLaunchKernelGGL(stream2d_flags<6>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 7: hipLaunchKernelGGL(stream2d_flags<7>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 8: hipLaunchKernelGGL(stream2d_flags<8>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -434,12 +456,12 @@ static const void *s2d_fn() {
 // Launch forms (cfg; one wave per workgroup in all of them -- four-wave
 // workgroups on adjacent strips lost their A/B, profiles/r02/ab_cfg_s5.log):
 //   0 plain stores, 3 non-temporal lattice stores, 4 LP (older rows of
-//   planes 2, 5, 6 in LDS; S = 6 only: the default form at S = 6, where the
-//   plain form runs out of registers; at S = 5 the two forms measure equal,
-//   profiles/r03/ab_forms_s5_s6.log).
+//   planes 2, 5, 6 and the |u| sums in LDS; bitwise S = 6, the default form
+//   at S = 6, where the plain form runs out of registers -- at S = 5 the two
+//   forms measure equal, profiles/r03/ab_forms_s5_s6.log; tolerance S = 6..8).
 // tol: the LBM_FLAG_TOLERANCE collision (collide2t) in forms 0 and 4.
-static bool s2d_form_ok(int steps, int cfg, bool tol) {
-    if (cfg == 4) return steps == 6;
+bool s2d_form_ok(int steps, int cfg, bool tol) {
+    if (cfg == 4) return steps == 6 || (tol && (steps == 7 || steps == 8));
     if (cfg == 0) return steps >= 2 && steps <= 6;
     if (cfg == 3) return !tol && steps >= 2 && steps <= 6;
     return false;
@@ -452,6 +474,8 @@ hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
     const void *fn = nullptr;
     if (cfg == 4) {
         switch (steps) {
+            case 7: fn = s2d_fn<7, true, true>(); break;
+            case 8: fn = s2d_fn<8, true, true>(); break;
             default: fn = tol ? s2d_fn<6, true, true>() : s2d_fn<6, false, true>(); break;
         }
     } else {  // cfg 3 has the registers of cfg 0
@@ -472,6 +496,8 @@ hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduc
         switch (steps * 2 + (tol ? 1 : 0)) {
             case 12: launch_s2d<6, false, false, true>(a, units, reduce, s); break;
             case 13: launch_s2d<6, false, true, true>(a, units, reduce, s); break;
+            case 15: launch_s2d<7, false, true, true>(a, units, reduce, s); break;
+            case 17: launch_s2d<8, false, true, true>(a, units, reduce, s); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

@@ -334,6 +334,50 @@ def test_stream_segments_bitwise(gpu_lib, S, cfg, hs, monkeypatch):
             np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(parts=4, grid=(2, 2)), dict(parts=2, grid=(1, 2), transport="rccl")])
+def test_stream_fused_remainder_bitwise(gpu_lib, kw):
+    """A run of K = 6q + r steps on the S = 6 stream kernel is q fused launches
+    plus, for r >= 2, ONE fused launch of r steps (its halo cells go to the
+    innermost r ghost columns / rows of the 6-deep ring; the ring is rebuilt
+    after it) -- bitwise vs the oracle for r = 0..5, single domain, 2x2
+    loop-back, and every wrap through RCCL (forced exchange)."""
+    kw = dict(kw)
+    if kw.pop("transport", None) == "rccl":
+        kw = dict(transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1, unique_id=gpu_lib.rccl_unique_id(),
+                  flags=gpu_lib.FLAG_FORCE_EXCHANGE)
+    p, obst = load_problem("128x256", iters=17)
+    cells0 = lio.init_cells(p)
+    with gpu_lib.Engine(p, obst, devices=[0], kernel=gpu_lib.KERNEL_STREAM, steps_per_launch=6, **kw) as e:
+        e.load_cells(cells0)
+        done = 0
+        for r in range(6):  # consecutive runs continue the state (accelerate once, first)
+            steps = 6 + r
+            e.run_steps(steps, accelerate_first=done == 0)
+            assert e.run_stats() == (1 + (r >= 2), 1 if r == 1 else 0), r
+            done += steps
+            cells, av = e.store(n_av=steps)
+            ref, _ = oracle.run(p, obst, done, cells0)
+            assert np.array_equal(cells, ref), (r, done)
+
+
+def test_8192_fused_remainder_vs_oracle(gpu_lib):
+    """The headline engine (auto = stream, S = 6, placement probe on) over
+    16 steps = two 6-step launches + one fused 4-step launch, bitwise vs the
+    oracle at 8192^2."""
+    n = 8192
+    p = lio.Params(n, n, 16, 10, 0.1, 0.005, 1.85)
+    obst = bench_obstacles(n)
+    with gpu_lib.Engine(p, obst) as e:
+        assert e.kernel_in_use() == "stream" and e.steps_per_launch() == 6
+        e.init_equilibrium()
+        e.run_steps(16, accelerate_first=True)
+        assert e.run_stats() == (3, 0)
+        cells, av = e.store(n_av=16)
+    ref, ref_av = oracle.run_mt(p, obst, 16, 16, lio.init_cells(p))
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=2e-3)
+
+
 def test_16384_single_domain_vs_oracle(gpu_lib):
     """BASELINE config 4's grid on one GPU with the headline kernel (auto =
     stream, LP form, S = 6, placement probe on): 7 steps = one fused 6-step
