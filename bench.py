@@ -380,21 +380,32 @@ def multi_rank_check(rank: int, world: int, local_rank: int, n: int = 2048, step
     return {"passed": bool(ok[0]), "grid": f"{n}x{n}", "steps": steps, "cases": results}
 
 
-# Device ms per launch at 8192^2 (profiles/r03/): fused 6-step and 5-step
-# stream launches, and the one-step launch a remainder of K % S steps costs.
-LAUNCH_MS = {6: 1.41, 5: 1.22, 1: 0.81}
+# Device ms per fused launch of S steps at 8192^2 (profiles/r03/deep_tol/,
+# profiles/r03/ab_forms_s5_s6.log): bitwise and tolerance collision; a launch
+# of 2..4 steps is bound by the lattice pass (~1.2 ms); a one-step (vec4)
+# launch 0.81 ms.
+LAUNCH_MS = {"bitwise": {2: 1.15, 3: 1.18, 4: 1.2, 5: 1.24, 6: 1.43},
+             "tolerance": {2: 1.15, 3: 1.18, 4: 1.2, 5: 1.21, 6: 1.2, 7: 1.22, 8: 1.47}}
+ONE_STEP_MS = 0.81
 
 
-def pick_spl(steps: int, requested: int) -> int:
+def pick_spl(steps: int, requested: int, numerics: str = "bitwise", fused_remainder: bool = True) -> int:
     """Steps per fused launch for a timed run of `steps` steps: the caller's
-    choice if given, else whichever of the library's two fastest forms (S = 6,
-    S = 5) finishes `steps` sooner once the one-step launches of a remainder
-    (steps % S) are counted -- the driver's 20-step run is four 5-step
-    launches, a 1000-step run 166 six-step launches plus four one-step ones."""
+    choice if given, else the S whose launches finish `steps` soonest, counting
+    the remainder steps % S as the library runs it (include/lbm_hip.h: one
+    fused launch when >= 2 steps, else one one-step launch) -- bitwise: the
+    driver's 20-step run is four 5-step launches, 1000 steps 166 six-step
+    launches + a 4-step one; tolerance: 7 + 7 + 6 and 142 x 7 + 6."""
     if requested:
         return requested
-    est = {S: (steps // S) * LAUNCH_MS[S] + (steps % S) * LAUNCH_MS[1] for S in (6, 5)}
-    return min(est, key=lambda S: (est[S], -S))
+    ms = LAUNCH_MS[numerics]
+
+    def est(S):
+        r = steps % S
+        tail = ms[r] if (r >= 2 and fused_remainder) else r * ONE_STEP_MS
+        return (steps // S) * ms[S] + tail
+
+    return min(sorted(ms, reverse=True), key=est) if steps > 0 else max(ms)
 
 
 def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: int, rank: int, world: int,
@@ -411,11 +422,12 @@ def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: 
         box = [native.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
+    numerics = "tolerance" if kflags & native.FLAG_TOLERANCE else "bitwise"
+    spl = pick_spl(args.steps, args.spl, numerics) if kernel in (native.KERNEL_AUTO, native.KERNEL_STREAM) else args.spl
     eng = native.Engine(p, obst, parts=world, grid=(R, C),
                         transport=native.TRANSPORT_RCCL if dist_on else native.TRANSPORT_LOCAL,
                         rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel, flags=kflags,
-                        steps_per_launch=pick_spl(args.steps, args.spl) if kernel in (native.KERNEL_AUTO,
-                                                                                       native.KERNEL_STREAM) else args.spl)
+                        steps_per_launch=spl)
     try:
         eng.init_equilibrium()
         spl = eng.steps_per_launch()
@@ -456,6 +468,22 @@ def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: 
                                   "(tools/settle_probe.py); untimed, same count on every rank"}}
     finally:
         eng.close()
+
+
+TOLERANCE_NOTE = ("LBM_FLAG_TOLERANCE (include/lbm_hip.h): IEEE fp32, one reciprocal of rho per cell (v_rcp_f32 + a "
+                  "Newton step) and FMA-reassociated BGK terms instead of LastChance.cpp's two correctly rounded "
+                  "divisions; stated tolerance (tests/test_gpu_tolerance.py): every population within 2e-5 "
+                  "relative of the CPU oracle after 100 steps at 8192^2 and after 20 steps with S = 8, av_vels "
+                  "within 2e-3, check.py (1 %) passes on all four reference grids at full maxIters, and the "
+                  "lattice does not depend on steps per launch or decomposition")
+
+
+def launch_plan(steps: int, spl: int, stream: bool) -> str:
+    """The launches a run of `steps` steps makes (include/lbm_hip.h)."""
+    q, r = divmod(steps, spl)
+    if r >= 2 and stream:
+        return f"{q} x {spl} + 1 x {r} (fused remainder)"
+    return f"{q} x {spl}" + (f" + {r} x 1" if r else "")
 
 
 WATCHDOG_EXIT = 3
@@ -514,7 +542,13 @@ def main() -> int:
     ap.add_argument("--kernel", default="auto", choices=["auto", "resident", "stream", "step2", "vec4", "scalar", "pipeline"],
                     help="stream: fused S-step register-streaming kernel; step2: fused two-step LDS kernel; "
                          "vec4/scalar: one step per launch; auto: the library's choice")
-    ap.add_argument("--spl", type=int, default=0, help="stream: time steps per launch (2..6; 0 = library default, 6)")
+    ap.add_argument("--spl", type=int, default=0,
+                    help="stream: time steps per launch (2..6, 2..8 with tolerance numerics; 0 = the fastest for "
+                         "--steps by the measured launch times, pick_spl)")
+    ap.add_argument("--numerics", default="tolerance", choices=["tolerance", "bitwise"],
+                    help="value's collision: tolerance = LBM_FLAG_TOLERANCE (fp32, within the stated tolerance of "
+                         "the reference: north_star's 'within a stated fp32 tolerance'); bitwise = every population "
+                         "bit-identical to LastChance.cpp; the other mode is measured too (aux)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true")
     ap.add_argument("--no-d3q19", action="store_true")
@@ -553,22 +587,29 @@ def main() -> int:
         except Exception as exc:  # recorded, never silently dropped
             mrc = {"passed": False, "error": str(exc)}
         log(f"multi-rank bitwise check: {mrc}")
-    m = measure_weak(tnx, tny, R, C, args, kernel, kflags, rank, world, local_rank, dist_on)
+    tol_main = args.numerics == "tolerance" and args.kernel in ("auto", "stream")
+    kflags_main = kflags | (native.FLAG_TOLERANCE if tol_main else 0)
+    m = measure_weak(tnx, tny, R, C, args, kernel, kflags_main, rank, world, local_rank, dist_on)
     nx, ny, elapsed, dev_secs = m["nx"], m["ny"], m["elapsed"], m["dev_secs"]
     kernel_used, steps_per_launch = m["kernel"], m["spl"]
 
     total_cells = nx * ny
     value = total_cells * args.steps / elapsed / 1e6
-    # a fused launch advances steps_per_launch time steps and moves the
+    # every launch (fused S steps, a fused remainder, or one step) moves the
     # lattice through HBM once: 72 algorithmic bytes per cell per launch
-    launches = max(args.steps // steps_per_launch, 1)
+    launches = max(m["launches"][0] + m["launches"][1], 1)
     per_launch_s = dev_secs / launches
     cells_per_gpu = tnx * tny
     achieved = BYTES_PER_UPDATE * cells_per_gpu / per_launch_s / 1e9
-    effective = achieved * steps_per_launch
-    wl_key = f"{tnx}x{tny}/{kernel_used}" + (str(steps_per_launch) if kernel_used == "stream" else "")
+    effective = BYTES_PER_UPDATE * cells_per_gpu * args.steps / dev_secs / 1e9
+    wl_key = (f"{tnx}x{tny}/{kernel_used}" + (str(steps_per_launch) if kernel_used == "stream" else "") +
+              ("t" if m["numerics"] == "tolerance" else ""))
     prof = load_traffic(wl_key)
     traffic = prof.get("hbm_bytes_per_launch")
+    valu = prof.get("valu") or {}
+    # the bound that binds: the VALU pipe when the profile
+    # of this kernel shows it busy most of the time, else the lattice pass
+    bound = "valu" if valu.get("busy_frac", 0) >= 0.75 else "hbm"
 
     out = {
         "metric": METRIC,
@@ -589,7 +630,7 @@ def main() -> int:
                                    f"exchange overlapped with the interior" if n > 1 else "single GPU"),
                    "kernel": kernel_used},
         "settle": m["settle"],
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": BYTES_PER_UPDATE * cells_per_gpu,
                      "cell_updates_per_launch": steps_per_launch * cells_per_gpu,
@@ -599,33 +640,40 @@ def main() -> int:
                      # the lattice through HBM once per S updates, so this can exceed the peak
                      "effective_gbs": round(effective, 1),
                      "effective_frac": round(effective / HBM_PEAK_GBS, 4),
-                     # the bound that binds: the VALU pipe, from the same profile
-                     "valu": prof.get("valu"), "profile": prof.get("profile")},
+                     # VALU instructions per launch and the pipe's busy fraction, same profile
+                     "valu": prof.get("valu") or None, "profile": prof.get("profile")},
         "av_vels_finite": m["finite"],
         "numerics": m["numerics"],
-        "launches": {"fused": m["launches"][0], "one_step": m["launches"][1]},
+        "launches": {"fused": m["launches"][0], "one_step": m["launches"][1],
+                     "plan": launch_plan(args.steps, steps_per_launch, kernel_used == "stream")},
     }
+    if m["numerics"] == "tolerance":
+        out["tolerance"] = TOLERANCE_NOTE
     if mrc is not None:
         out["multi_rank_bitwise"] = bool(mrc.get("passed"))
         out["multi_rank_check"] = mrc
     aux = out.setdefault("aux", {})
     watchdog = AuxWatchdog(args.aux_budget, out, rank)
     if not args.no_aux and args.kernel in ("auto", "stream") and kernel_used == "stream":
-        # LBM_FLAG_TOLERANCE (include/lbm_hip.h): the reciprocal collision, same workload
+        # the same workload and step count with the other collision: bitwise
+        # (LastChance.cpp arithmetic) when `value` is the tolerance mode, and
+        # vice versa (LBM_FLAG_TOLERANCE, include/lbm_hip.h)
+        other = "bitwise" if m["numerics"] == "tolerance" else "tolerance"
         try:
-            mt = measure_weak(tnx, tny, R, C, args, kernel, kflags | native.FLAG_TOLERANCE, rank, world, local_rank,
-                              dist_on)
-            lt = mt["dev_secs"] / max(mt["launches"][0], 1)
-            aux[f"stream{mt['spl']}_tolerance"] = {
+            mt = measure_weak(tnx, tny, R, C, args, kernel, kflags | (native.FLAG_TOLERANCE if other == "tolerance"
+                                                                     else 0), rank, world, local_rank, dist_on)
+            lt = mt["dev_secs"] / max(mt["launches"][0] + mt["launches"][1], 1)
+            aux[f"stream{mt['spl']}_{other}"] = {
                 "mlups": round(mt["nx"] * mt["ny"] * args.steps / mt["elapsed"] / 1e6, 1),
                 "ms_per_step": round(mt["elapsed"] / args.steps * 1e3, 5), "numerics": mt["numerics"],
+                "steps_per_launch": mt["spl"], "launches": launch_plan(args.steps, mt["spl"], True),
                 "avg_launch_ms": round(lt * 1e3, 5),
                 "hbm_frac_per_pass": round(BYTES_PER_UPDATE * tnx * tny / lt / 1e9 / HBM_PEAK_GBS, 4),
-                "tolerance": "LBM_FLAG_TOLERANCE: one reciprocal of rho per cell, FMA contraction; check.py passes "
-                             "on all four reference grids, populations within 2e-5 relative of the oracle after "
-                             "100 steps at 8192^2 (tests/test_gpu_tolerance.py)"}
+                **({"tolerance": TOLERANCE_NOTE} if other == "tolerance" else
+                   {"parity": "every population bit-identical to the CPU oracle (LastChance.cpp:226-262 restated), "
+                              "tests/test_gpu_parity.py"})}
         except Exception as exc:
-            aux["stream_tolerance"] = {"error": str(exc)}
+            aux[f"stream_{other}"] = {"error": str(exc)}
     if n > 1 and not args.no_aux:
         try:
             ms = measure_weak(tnx, tny, n, 1, args, kernel, kflags, rank, world, local_rank, dist_on)

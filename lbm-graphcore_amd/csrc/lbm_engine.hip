@@ -199,7 +199,10 @@ struct lbm_handle {
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     int stream_cfg = 4;      // LBM_STREAM_CFG (launch form, one wave per workgroup): 0 plain stores;
                              // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 8)
-    int tol_s = 6, tol_cfg = 4;  // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
+    // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
+    // (S = 7, LP form: 386 vs 336 GLUPS at S = 6 and 365 at S = 8, which spills;
+    // profiles/r03/deep_tol/ab96.log)
+    int tol_s = 7, tol_cfg = 4;
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)

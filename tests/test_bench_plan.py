@@ -1,0 +1,34 @@
+"""bench.py's choice of steps per launch (CPU only): pick_spl uses the
+measured launch times and counts a remainder as the library runs it (one
+fused launch of >= 2 steps, include/lbm_hip.h)."""
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "lbm-graphcore_amd")]
+
+import bench  # noqa: E402
+
+
+def test_pick_spl_driver_and_default_runs():
+    assert bench.pick_spl(20, 0, "bitwise") == 5        # 4 x 5
+    assert bench.pick_spl(20, 0, "tolerance") == 7      # 7 + 7 + 6
+    assert bench.pick_spl(1000, 0, "bitwise") == 6      # 166 x 6 + 4
+    assert bench.pick_spl(1000, 0, "tolerance") == 7    # 142 x 7 + 6
+    assert bench.pick_spl(20, 4, "tolerance") == 4      # the caller's choice wins
+
+
+def test_pick_spl_every_step_count_is_valid():
+    for numerics, smax in (("bitwise", 6), ("tolerance", 8)):
+        for steps in range(0, 200):
+            S = bench.pick_spl(steps, 0, numerics)
+            assert 2 <= S <= smax
+
+
+def test_launch_plan_strings():
+    assert bench.launch_plan(20, 7, True) == "2 x 7 + 1 x 6 (fused remainder)"
+    assert bench.launch_plan(13, 6, True) == "2 x 6 + 1 x 1"
+    assert bench.launch_plan(20, 5, True) == "4 x 5"
+    assert bench.launch_plan(7, 2, False) == "3 x 2 + 1 x 1"

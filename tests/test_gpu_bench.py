@@ -36,8 +36,18 @@ def test_bench_json_contract():
     assert "vs_baseline" in d and d["vs_baseline"] is None
     assert "workload" in d["config"] and "8192x8192" in d["config"]["workload"]
     r = d["roofline"]
-    assert r["bound"] in ("hbm", "mfma") and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    # "valu" where the committed PMC profile of the kernel shows the VALU pipe
+    # binding; achieved / peak / frac stay the HBM roofline
+    assert r["bound"] in ("hbm", "valu") and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert d["numerics"] in ("bitwise", "tolerance") and (d["numerics"] == "bitwise" or "tolerance" in d)
     assert 0 < r["frac"] < 1 and r["achieved"] == pytest.approx(r["frac"] * r["peak"], rel=1e-3)
     # value (whole-job MLUPS) and ms_per_step describe the same timed region
     assert d["value"] == pytest.approx(8192 * 8192 / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
     assert d["av_vels_finite"] is True
+
+
+def test_bench_bitwise_numerics_line():
+    d = run_bench("--steps", "14", "--warmup", "2", "--no-cpu-baseline", "--no-aux", "--numerics", "bitwise")
+    assert d["numerics"] == "bitwise" and "tolerance" not in d
+    assert d["launches"]["plan"] in ("2 x 6 + 1 x 2 (fused remainder)", "2 x 5 + 1 x 4 (fused remainder)",
+                                     "2 x 7", "3 x 4 + 1 x 2 (fused remainder)")

@@ -5,8 +5,8 @@
 # SQ counters, each in its own run) of the default kernel at 8192^2.
 #   /usr/local/graft/bin/gpurun --timeout 1500 -- bash tools/gpu_round.sh
 # then: python3 tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch/fetch_counter_collection.csv \
-#         --write gpurun_out/pmc_write/write_counter_collection.csv --kernel "stream_steps2d<6" \
-#         --sq gpurun_out/pmc_sq/sq_counter_collection.csv --key 8192x8192/stream6 --cells 67108864 \
+#         --write gpurun_out/pmc_write/write_counter_collection.csv --kernel "stream_steps2d<7" \
+#         --sq gpurun_out/pmc_sq/sq_counter_collection.csv --key 8192x8192/stream7t --cells 67108864 \
 #         --profile "profiles/rNN/...: kernel, date" --out profiles/traffic.json
 # The pytest step continues on test FAILURES (exit 1: the rest still runs, the
 # log says what failed) but stops on anything else (crash, abort, timeout).
@@ -19,7 +19,7 @@ bash tools/gpu_steps.sh \
   "400|bench_drv|python3 bench.py --gpus 1 --steps 20 --warmup 5" \
   "500|bench|python3 bench.py --no-cpu-baseline" \
   "300|prof_trace|rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o drv --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-aux" \
-  "120|pmc_fetch|timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1" \
-  "120|pmc_write|timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1" \
-  "120|pmc_sq|timeout -s KILL 100 rocprofv3 --pmc $SQ -d gpurun_out/pmc_sq -o sq --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1"
+  "120|pmc_fetch|timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1 --variant tol:FLAGS=4" \
+  "120|pmc_write|timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1 --variant tol:FLAGS=4" \
+  "120|pmc_sq|timeout -s KILL 100 rocprofv3 --pmc $SQ -d gpurun_out/pmc_sq -o sq --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1 --variant tol:FLAGS=4"
 grep -h "passed\|failed" gpurun_out/pytest_gpu.log; tail -n 2 gpurun_out/smoke.log; tail -n 1 gpurun_out/bench.log
