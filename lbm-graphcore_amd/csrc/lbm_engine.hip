@@ -197,6 +197,7 @@ struct lbm_handle {
     int stream_hs = 0;       // LBM_STREAM_HS: rows per stream segment (0 = by size)
     int og = 4;              // ghost width of the obstacle map
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
+    bool guide_set = false;                    // guide given by LBM_STREAM_GUIDE (else by S at create)
     int stream_cfg = 4;      // LBM_STREAM_CFG (launch form, one wave per workgroup): 0 plain stores;
                              // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 8)
     // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
@@ -273,6 +274,24 @@ struct lbm_handle {
         HIP_CHECK(hipStreamSynchronize(st));
     }
 
+    // LBM_STREAM_GUIDE tiers "h1:f1,h2:f2,...,hK" (see guided_rects); "0" = uniform
+    void set_guide(const std::string &spec) {
+        guide.clear();
+        guide_set = true;
+        if (spec == "0") return;
+        size_t pos = 0;
+        while (pos < spec.size()) {
+            size_t end = spec.find(',', pos);
+            if (end == std::string::npos) end = spec.size();
+            const std::string item = spec.substr(pos, end - pos);
+            const size_t c = item.find(':');
+            const int ht = atoi(item.substr(0, c).c_str());
+            const float fr = c == std::string::npos ? 1.f : (float)atof(item.substr(c + 1).c_str());
+            if (ht > 0) guide.emplace_back(ht, fr);
+            pos = end + 1;
+        }
+    }
+
     static int env_int(const char *name, int dflt) {
         const char *v = getenv(name);
         return (v && *v) ? atoi(v) : dflt;
@@ -300,24 +319,7 @@ struct lbm_handle {
         tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
         tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 8);
         stream_min_cells = std::max(0, knob("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
-        {
-            const char *g = knob_str("LBM_STREAM_GUIDE");
-            std::string spec = g ? std::string(g) : std::string("96:0.85,32:0.1,10");
-            guide.clear();
-            if (spec != "0") {
-                size_t pos = 0;
-                while (pos < spec.size()) {
-                    size_t end = spec.find(',', pos);
-                    if (end == std::string::npos) end = spec.size();
-                    const std::string item = spec.substr(pos, end - pos);
-                    const size_t c = item.find(':');
-                    const int ht = atoi(item.substr(0, c).c_str());
-                    const float fr = c == std::string::npos ? 1.f : (float)atof(item.substr(c + 1).c_str());
-                    if (ht > 0) guide.emplace_back(ht, fr);
-                    pos = end + 1;
-                }
-            }
-        }
+        if (const char *g = knob_str("LBM_STREAM_GUIDE")) set_guide(g);
         res_th_env = std::max(0, knob("LBM_RES_TH", 0));
         res_version = knob("LBM_RES_V", 0);
         res_per_cu = std::min(std::max(knob("LBM_RES_PER_CU", res_per_cu), 1), 2);
@@ -881,6 +883,10 @@ struct lbm_handle {
         use_stream = kernel == LBM_KERNEL_STREAM || (kernel == LBM_KERNEL_AUTO && can_stream && big);
         spl = use_stream ? S : 2;
         hw = spl;
+        // default segment tiers by S (2S rows re-streamed per segment): S <= 6
+        // 96/32/10 (profiles/r02/ab_guide_tiers.log), S >= 7 144/48/16
+        // (profiles/r03/guide7/: 400 vs 390 GLUPS at 98 steps, 385 vs 377 at 20)
+        if (!guide_set) set_guide(spl >= 7 ? "144:0.85,48:0.1,16" : "96:0.85,32:0.1,10");
         gr = std::max(2, hw);
         og = gr + 2;  // the two-column stream kernel's strips start up to S+1 columns left of their first cell
 

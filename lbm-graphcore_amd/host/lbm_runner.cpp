@@ -36,7 +36,10 @@ void usage(const char *exe) {
               << "      --runs arg       timed re-runs after the first (default: 5)\n"
               << "      --kernel arg     auto, resident, stream, step2, vec4, scalar or pipeline (default: auto; vec4/scalar = one\n"
               << "                       step per launch; pipeline = unfused per-stage kernels)\n"
-              << "      --spl arg        stream kernel: time steps per launch, 2..6 (default: library choice, 6)\n"
+              << "      --spl arg        stream kernel: time steps per launch, 2..6, 2..8 with --tolerance (default:\n"
+              << "                       library choice, 6; 7 with --tolerance)\n"
+              << "      --tolerance      fp32 tolerance-mode collision (LBM_FLAG_TOLERANCE: one reciprocal of rho per\n"
+              << "                       cell; not bit-identical to the reference, within the tolerance lbm_hip.h states)\n"
               << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n"
               << "      --graph-steps arg  replay the step loop as hipGraphs of 2*arg launches (0 = library default, <0 = off)\n"
               << "      --dump-partitioning arg  write the sub-domain decomposition as JSON\n";
@@ -48,7 +51,7 @@ int main(int argc, char *argv[]) {
     std::string paramsFile, obstaclesFile, device = "gpu", exeFile, kernel = "auto", outDir = ".", dumpFile;
     int spl = 0;
     int numGpus = 1, runs = 5, graphSteps = 0;
-    bool debug = false;
+    bool debug = false, tolerance = false;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         std::string val;
@@ -90,6 +93,8 @@ int main(int argc, char *argv[]) {
             std::string v;
             if (!next(v)) { usage(argv[0]); return EXIT_FAILURE; }
             spl = std::atoi(v.c_str());
+        } else if (a == "--tolerance") {
+            tolerance = true;
         } else if (a == "--out-dir") {
             if (!next(outDir)) { usage(argv[0]); return EXIT_FAILURE; }
         } else if (a == "--graph-steps") {
@@ -180,6 +185,7 @@ int main(int argc, char *argv[]) {
                    : kernel == "pipeline" ? LBM_KERNEL_PIPELINE
                                         : LBM_KERNEL_AUTO;
         if (kernel == "scalar" || kernel == "vec4") cfg.flags |= LBM_FLAG_ONE_STEP;
+        if (tolerance) cfg.flags |= LBM_FLAG_TOLERANCE;
         cfg.steps_per_launch = spl;
         cfg.graph_steps = graphSteps;
         lbmhost::check(lbm_create_ex(&abi, obstacles->data.data(), &cfg, &h), nullptr, "lbm_create_ex");

@@ -31,7 +31,10 @@ def _gate(tmp_path, grid):
                                   ["-n", "1", "--kernel", "stream", "--spl", "3"],
                                   ["-n", "4", "--device", "loopback", "--kernel", "stream"],
                                   ["-n", "1", "--kernel", "resident"],
-                                  ["-n", "2", "--device", "loopback", "--kernel", "pipeline"]])
+                                  ["-n", "2", "--device", "loopback", "--kernel", "pipeline"],
+                                  ["-n", "1", "--kernel", "stream", "--tolerance"],
+                                  ["-n", "2", "--device", "loopback", "--kernel", "stream", "--tolerance",
+                                   "--spl", "8"]])
 def test_lbm_runner_128(gpu_lib, tmp_path, args):
     exe = PKG / "build" / "lbm_runner"
     r = subprocess.run([str(exe), "--params", str(GOLD / "params" / "input_128x128.params"),
@@ -47,7 +50,8 @@ def test_lbm_runner_128(gpu_lib, tmp_path, args):
         m = json.loads((GOLD / "oracle_pipe" / "128x128.json").read_text())
     else:
         m = oracle_manifest("128x128")
-    assert re_out == pytest.approx(m["reynolds_last_av"], rel=2e-4)
+    # tolerance mode: the reciprocal collision, within its stated tolerance of the oracle
+    assert re_out == pytest.approx(m["reynolds_last_av"], rel=2e-3 if "--tolerance" in args else 2e-4)
     res = _gate(tmp_path, "128x128")
     assert res["passed"], res
 

@@ -1,6 +1,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
+G="--variant g96:FLAGS=4 --variant g128:FLAGS=4,LBM_STREAM_GUIDE=128:0.8,48:0.15,16 --variant g144:FLAGS=4,LBM_STREAM_GUIDE=144:0.85,48:0.1,16 --variant g192:FLAGS=4,LBM_STREAM_GUIDE=192:0.75,64:0.15,24 --variant g120:FLAGS=4,LBM_STREAM_GUIDE=120:0.9,40 --variant g112:FLAGS=4,LBM_STREAM_GUIDE=112:0.85,40:0.1,14"
 bash tools/gpu_steps.sh \
-  "600|t_new|python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_gpu_tolerance.py tests/test_gpu_parity.py -k 'tolerance or remainder or segments or forced_exchange or large_grid'" \
-  "400|ab96|python3 tools/ab_bench.py --n 8192 --steps 96 --warmup 12 --rounds 3 --variant base: --variant s5:LBM_STREAM_S=5 --variant tol6:FLAGS=4 --variant tol7:FLAGS=4,LBM_TOL_S=7 --variant tol8:FLAGS=4,LBM_TOL_S=8" \
-  "300|ab20|python3 tools/ab_bench.py --n 8192 --steps 20 --warmup 5 --rounds 3 --variant s5:LBM_STREAM_S=5 --variant tol5:FLAGS=4,LBM_TOL_S=5 --variant tol7:FLAGS=4,LBM_TOL_S=7 --variant tol8:FLAGS=4,LBM_TOL_S=8"
-grep -h "passed\|failed" gpurun_out/t_new.log | tail -3; cat gpurun_out/ab96.log gpurun_out/ab20.log | grep variant
+  "400|ab_guide7|python3 tools/ab_bench.py --n 8192 --steps 98 --warmup 14 --rounds 3 $G" \
+  "300|ab_guide7_20|python3 tools/ab_bench.py --n 8192 --steps 20 --warmup 5 --rounds 3 $G"
+cat gpurun_out/ab_guide7.log gpurun_out/ab_guide7_20.log | grep variant
