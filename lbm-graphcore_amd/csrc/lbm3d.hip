@@ -401,16 +401,18 @@ __global__ __launch_bounds__(B3X * B3Y) void step3d_pair(Step3Args a, int planes
 //   own row, x +- 1 by DPP:   speeds 0,1,2 of plane z, 9,10,11 of plane z-1
 //                             (registers kept from earlier iterations),
 //                             14,15,16 of plane z+1;
-//   rows y +- 1 through LDS:  3..8 of plane z (ring of 2 plane slots),
+//   rows y +- 1 through LDS:  3..8 of plane z (one slot set, read into
+//                             registers the iteration plane z arrives),
 //                             12,13 of plane z-1 (ring of 3), 17,18 of z+1.
 // Two barriers per iteration (one per level) order every slot's writes and
 // reads (each slot is rewritten only after the barrier that follows its last
-// read).  Algorithmic traffic per cell update: (19 loads x 768/480 + 19
-// stores) x 4 B / 2 = 99 B instead of 152.  Same cell3d arithmetic: bitwise
-// equal to the one-step kernels.
+// read).  Algorithmic traffic per cell update: (19 loads x 64 TH / (60 (TH-4))
+// + 19 stores) x 4 B / 2 = 98.8 B at TH = 12, 92.3 B at TH = 16, instead of
+// 152.  Same cell3d arithmetic: bitwise equal to the one-step kernels.
 // ---------------------------------------------------------------------------
 // TH = rows per block (waves), a template parameter (LBM3D_TH): two levels of
-// 20 plane slots of 64 x TH floats take 10 x TH KB of LDS (TH <= 15).
+// 14 plane slots of 64 x TH floats take 7 x TH KB of LDS (TH <= 16: one
+// block of 16 waves per CU, 4 per SIMD).
 // SKIP: a wave whose row no level-2 (level-1) cell depends on skips that
 // level's collision (rows 0 and TH-1 at level 1; rows 0, 1, TH-2, TH-1 at
 // level 2) -- it still writes and reads its LDS slots and barriers, and the
@@ -418,10 +420,16 @@ __global__ __launch_bounds__(B3X * B3Y) void step3d_pair(Step3Args a, int planes
 // rows 1 .. TH-2).
 constexpr int T3W = 64;
 constexpr int T3OX = T3W - 4;  // owned columns
+// Z (speeds 3..8 of the newest plane) is single-buffered: each thread reads
+// its six y +- 1 pulls right after the barrier that publishes them and keeps
+// them in registers (zr) until the next iteration, when that plane is the
+// centre plane -- 14 slots per level instead of 20 (round 3), so blocks of
+// 16 rows fit (owned 60 x 12 of 64 x 16 loaded: 92 B per update instead of
+// 98.8 for 12 rows).
 template <int TH>
 struct T3 {
     static constexpr int C = T3W * TH;                    // cells per plane slot
-    static constexpr int LDS = (2 + 2 * 6 + 3 * 2) * C;   // floats per level: M, Z[2][6], P[3][2]
+    static constexpr int LDS = (2 + 6 + 3 * 2) * C;       // floats per level: M, Z[6], P[3][2]
     static constexpr int OY = TH - 4;                     // owned rows
 };
 
@@ -443,33 +451,36 @@ struct Two3Args {
 // later level or output needs this row's result.
 template <int TH, bool TOL>
 __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3], float *lds, int jz, float (&r0)[3],
-                                        float (&r9a)[3], float (&r9b)[3], int lane, int wy, bool ob, bool live,
-                                        const Two3Args &a) {
+                                        float (&r9a)[3], float (&r9b)[3], float (&zr)[6], int lane, int wy, bool ob,
+                                        bool live, const Two3Args &a) {
     constexpr int T3C = T3<TH>::C;
-    float *M = lds, *Z = lds + 2 * T3C, *P = lds + 14 * T3C;
+    float *M = lds, *Z = lds + 2 * T3C, *P = lds + 8 * T3C;
     const int c = wy * T3W + lane;
-    const int zw = jz & 1, pw = ((jz % 3) + 3) % 3;  // slots of plane jz
+    const int pw = ((jz % 3) + 3) % 3;  // P slot of plane jz
     M[c] = in[17];
     M[T3C + c] = in[18];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) Z[(zw * 6 + i) * T3C + c] = in[3 + i];
+    for (int i = 0; i < 6; ++i) Z[i * T3C + c] = in[3 + i];
     P[(pw * 2) * T3C + c] = in[12];
     P[(pw * 2 + 1) * T3C + c] = in[13];
     __syncthreads();
     const int wm = max(wy - 1, 0) * T3W, wp = min(wy + 1, TH - 1) * T3W;
     const int lm = max(lane - 1, 0), lp = min(lane + 1, T3W - 1);
-    const float *z = Z + ((jz - 1) & 1) * 6 * T3C;          // plane jz - 1
     const float *p = P + ((((jz - 2) % 3) + 3) % 3) * 2 * T3C;  // plane jz - 2
     float s[Q3];
     s[0] = r0[0];
     s[1] = dpp_from_left(r0[1]);
     s[2] = dpp_from_right(r0[2]);
-    s[3] = z[0 * T3C + wm + lane];
-    s[4] = z[1 * T3C + wp + lane];
-    s[5] = z[2 * T3C + wm + lm];
-    s[6] = z[3 * T3C + wp + lp];
-    s[7] = z[4 * T3C + wp + lm];
-    s[8] = z[5 * T3C + wm + lp];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) s[3 + i] = zr[i];  // plane jz - 1's pulls, read one iteration ago
+    // plane jz's y +- 1 pulls of speeds 3..8, for the next iteration (the slot
+    // is rewritten only after the next barrier of this level's other half)
+    zr[0] = Z[0 * T3C + wm + lane];
+    zr[1] = Z[1 * T3C + wp + lane];
+    zr[2] = Z[2 * T3C + wm + lm];
+    zr[3] = Z[3 * T3C + wp + lp];
+    zr[4] = Z[4 * T3C + wp + lm];
+    zr[5] = Z[5 * T3C + wm + lp];
     s[9] = r9b[0];
     s[10] = dpp_from_left(r9b[1]);
     s[11] = dpp_from_right(r9b[2]);
@@ -500,7 +511,10 @@ __device__ __forceinline__ float level3(const float (&in)[Q3], float (&out)[Q3],
 }
 
 // PD: input planes in flight -- 1: plane j+1 while j is computed; 2: also j+2
-// (19 more VGPRs; one 768..960-thread block per CU keeps few loads in flight).
+// (19 more VGPRs; one 768..960-thread block per CU keeps few loads in flight);
+// 0: plane j+1 is loaded into the input registers once level 1 has consumed
+// them, in flight across level 2 only (19 VGPRs fewer: blocks of 16 rows fit
+// 128 VGPRs).
 template <int TH, bool SKIP, int PD, bool TOL = false>
 __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
     __shared__ float lds1[T3<TH>::LDS], lds2[T3<TH>::LDS];
@@ -516,6 +530,7 @@ __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
     const long long row = (long long)y * a.px + x;
     float r0a[3] = {0.f, 0.f, 0.f}, r9aa[3] = {0.f, 0.f, 0.f}, r9ba[3] = {0.f, 0.f, 0.f};
     float r0b[3] = {0.f, 0.f, 0.f}, r9ab[3] = {0.f, 0.f, 0.f}, r9bb[3] = {0.f, 0.f, 0.f};
+    float zra[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, zrb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float u1 = 0.f, u2 = 0.f;
     auto obz = [&](int zz) {  // planes zs-4 .. ze are asked for; only zs-1 .. ze are used
         zz = min(max(zz, -2), a.nz + 1);
@@ -537,8 +552,9 @@ __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
     }
     for (int j = zs - 2; j <= ze + 1; ++j) {
         float nin[Q3];
-        const float *pn = a.fin + (long long)min(j + PD, ze + 1) * a.PL + row;
-        if (PD == 2) {
+        const float *pn = a.fin + (long long)min(j + (PD == 0 ? 1 : PD), ze + 1) * a.PL + row;
+        if (PD == 0) {
+        } else if (PD == 2) {
 #pragma unroll
             for (int k = 0; k < Q3; ++k) nin[k] = far[k];
 #pragma unroll
@@ -550,17 +566,23 @@ __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
         ob2 = ob1;
         ob1 = obz(j - 1);
         float o1[Q3], o2[Q3];
-        const float v1 = level3<TH, TOL>(in, o1, lds1, j, r0a, r9aa, r9ba, lane, wy, ob1, live1, a);
+        const float v1 = level3<TH, TOL>(in, o1, lds1, j, r0a, r9aa, r9ba, zra, lane, wy, ob1, live1, a);
         if (own && j - 1 >= zs && j - 1 < ze) u1 += v1;
-        const float v2 = level3<TH, TOL>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, lane, wy, ob2, live2, a);
+        if (PD == 0) {  // level 1 is done with plane j: its registers take plane j + 1
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) in[k] = pn[k * a.KS];
+        }
+        const float v2 = level3<TH, TOL>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, zrb, lane, wy, ob2, live2, a);
         if (own && j - 2 >= zs && j - 2 < ze) {
             u2 += v2;
             float *d = a.fout + (long long)(j - 2) * a.PL + row;
 #pragma unroll
             for (int k = 0; k < Q3; ++k) __builtin_nontemporal_store(o2[k], d + k * a.KS);
         }
+        if (PD != 0) {
 #pragma unroll
-        for (int k = 0; k < Q3; ++k) in[k] = nin[k];
+            for (int k = 0; k < Q3; ++k) in[k] = nin[k];
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -686,7 +708,10 @@ struct lbm3d_handle {
     int seg = 64;      // LBM3D_SEG: z planes per block of the two-step kernel (32-128 equal within noise at 512^3)
     int th = 12;       // LBM3D_TH: rows (waves) per block of the two-step kernel (12, 14, 15)
     bool skip = false; // LBM3D_SKIP: waves skip the collisions of rows no later level reads (not faster)
-    int pd = 1;        // LBM3D_PD: input planes in flight in the two-step kernel (1, 2)
+    // LBM3D_PD: input planes in flight in the two-step kernel -- 0 (default): the
+    // next plane loaded once level 1 has consumed the current one (44.7 vs
+    // 38.6-42.5 GLUPS at 512^3 for 1, profiles/r03/d3q19/ab_pd.log); 1, 2
+    int pd = 0;
     long long kspad = 0;  // LBM3D_KSPAD: floats appended to each speed plane (multiple of 64)
     const char *lattice_pad = nullptr;  // LBM_LATTICE_PAD (debug knob)
     bool poison = false;  // LBM_POISON=1: fresh allocations filled with NaN bytes
@@ -746,7 +771,7 @@ struct lbm3d_handle {
         if (tolerance) {  // the tolerance pass exists for the default block only
             th = 12;
             skip = false;
-            pd = 1;
+            pd = 0;
         }
         // the two-step kernel is instantiated for these (rows, skip, prefetch)
         // combinations only; anything else is rejected here, never launched as
@@ -889,10 +914,12 @@ struct lbm3d_handle {
     }
     // switch key of the instantiated step3d_two<TH, SKIP, PD> variants, -1 if none
     static int two_variant(int th, bool skip, int pd) {
-        if ((th != 12 && th != 14 && th != 15) || (pd != 1 && pd != 2)) return -1;
+        if ((th != 12 && th != 14 && th != 15 && th != 16) || pd < 0 || pd > 2) return -1;
+        if (pd == 0) return (th == 12 || th == 16) && !skip ? 100 + th : -1;  // late-load variants
         const int key = (th * 2 + (skip ? 1 : 0)) * 2 + (pd - 1);
         switch (key) {
-            case 48: case 49: case 50: case 51: case 56: case 58: case 59: case 60: case 62: case 63: return key;
+            case 48: case 49: case 50: case 51: case 56: case 58: case 59: case 60: case 62: case 63: case 64:
+                return key;
             default: return -1;
         }
     }
@@ -935,8 +962,8 @@ struct lbm3d_handle {
         a.blk0 = blk0;
         const dim3 g((p.nx + T3OX - 1) / T3OX, (p.ny + th - 5) / (th - 4), (zn - z0 + seg - 1) / seg);
         const dim3 b(T3W, th);
-        if (tolerance) {  // the default block only (12 rows, no skip, one plane prefetched)
-            hipLaunchKernelGGL((step3d_two<12, false, 1, true>), g, b, 0, st, a);
+        if (tolerance) {  // the default block only (12 rows, no skip, late load)
+            hipLaunchKernelGGL((step3d_two<12, false, 0, true>), g, b, 0, st, a);
             H3(hipGetLastError());
             return;
         }
@@ -951,6 +978,9 @@ struct lbm3d_handle {
             case 60: hipLaunchKernelGGL((step3d_two<15, false, 1>), g, b, 0, st, a); break;
             case 62: hipLaunchKernelGGL((step3d_two<15, true, 1>), g, b, 0, st, a); break;
             case 63: hipLaunchKernelGGL((step3d_two<15, true, 2>), g, b, 0, st, a); break;
+            case 64: hipLaunchKernelGGL((step3d_two<16, false, 1>), g, b, 0, st, a); break;
+            case 112: hipLaunchKernelGGL((step3d_two<12, false, 0>), g, b, 0, st, a); break;
+            case 116: hipLaunchKernelGGL((step3d_two<16, false, 0>), g, b, 0, st, a); break;
             default: throw fail3(LBM_E_INTERNAL, "unvalidated two-step variant");
         }
         H3(hipGetLastError());

@@ -1,7 +1,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
-V="--variant w1:FLAGS=4 --variant w2:FLAGS=4,LBM_TOL_CFG=5 --variant w4:FLAGS=4,LBM_TOL_CFG=6 --variant w2s8:FLAGS=4,LBM_TOL_CFG=5,LBM_TOL_S=8 --variant w4s8:FLAGS=4,LBM_TOL_CFG=6,LBM_TOL_S=8"
+export LBM_DEBUG_KNOBS=1
 bash tools/gpu_steps.sh \
-  "300|t_mw|python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_gpu_tolerance.py -k multiwave" \
-  "400|ab_mw|python3 tools/ab_bench.py --n 8192 --steps 98 --warmup 14 --rounds 3 $V" \
-  "300|ab_mw20|python3 tools/ab_bench.py --n 8192 --steps 20 --warmup 5 --rounds 3 $V"
-grep -h "passed\|failed" gpurun_out/t_mw.log | tail -2; cat gpurun_out/ab_mw.log gpurun_out/ab_mw20.log | grep variant
+  "600|t_3d|python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_d3q19.py -k block_rows" \
+  "400|b3d|for v in 12:1 16:0 12:0 12:1 16:0 12:0; do LBM3D_TH=\${v%:*} LBM3D_PD=\${v#*:} python3 tools/bench3d.py --n 512 --steps 20 --rounds 3 || exit 1; done"
+grep -h "passed\|failed" gpurun_out/t_3d.log | tail -2; cat gpurun_out/b3d.log | grep grid
