@@ -47,7 +47,6 @@ hipError_t launch_step2(const Step2Args &a, int blocks, bool reduce, hipStream_t
 hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s);
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n);
 bool s2d_form_ok(int steps, int cfg, bool tol);
-int s2d_form_waves(int cfg);
 hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, hipStream_t s);
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s);
 hipError_t launch_accelerate(float *f, const uint8_t *obst, long long P, int pitch, int w, int row, float w1,
@@ -315,7 +314,7 @@ struct lbm_handle {
         xoff = std::max(MAX_GR, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
         stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 6);
         stream_hs = std::max(0, knob("LBM_STREAM_HS", stream_hs));
-        auto form = [](int c, int dflt) { return (c == 0 || (c >= 3 && c <= 6)) ? c : dflt; };
+        auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
         stream_cfg = form(knob("LBM_STREAM_CFG", stream_cfg), stream_cfg);
         tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
         tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 8);
@@ -648,7 +647,7 @@ struct lbm_handle {
             if (!(so && atoi(so) == 0)) {
                 std::vector<uint8_t> fl((size_t)ni + nb);
                 HIP_CHECK(hipMemcpy(fl.data(), s.uobst, fl.size(), hipMemcpyDeviceToHost));
-                const int W = s2d_form_waves(stream_cfg);  // waves per workgroup of the launch form
+                const int W = 1;  // one wave per workgroup in every launch form
                 std::vector<int> perm((size_t)ni + nb);
                 auto order = [&](int off, int n) {
                     const int blocks = (n + W - 1) / W, q = blocks / 8, r = blocks % 8;
@@ -710,7 +709,7 @@ struct lbm_handle {
             if (occ == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev) == hipSuccess &&
                 per_cu > 0 && cus > 0) {
-                const long long cap = (long long)per_cu * s2d_form_waves(stream_cfg) * cus;  // waves
+                const long long cap = (long long)per_cu * cus;
                 const long long nseg_max = std::max<long long>(1, rows / (4LL * S));
                 const long long k_max = std::max<long long>(1, nseg_max * strips / cap);
                 const long long k = std::min<long long>(8, k_max);
@@ -869,9 +868,9 @@ struct lbm_handle {
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max) +
                                                  (tolerance ? "" : " (up to 8 with LBM_FLAG_TOLERANCE)"));
-        // the LP forms exist for S = 6 (bitwise) and 6..8 (tolerance); S = 7, 8 have only them
-        if (S > 6 && stream_cfg < 4) stream_cfg = 4;
-        if (!s2d_form_ok(S, stream_cfg, tolerance)) stream_cfg = S > 6 ? 4 : 0;
+        // the LP form exists for S = 6 (bitwise) and 6..8 (tolerance); S = 7, 8 have only it
+        if (S > 6) stream_cfg = 4;
+        if (!s2d_form_ok(S, stream_cfg, tolerance)) stream_cfg = 0;
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
         for (auto &r : all_rects) {
             const int mw = (C > 1 || force_exchange) ? 2 * S : S, mh = (R > 1 || force_exchange) ? 2 * S : S;

@@ -440,18 +440,17 @@ hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, h
     return hipGetLastError();
 }
 
-template <int S, bool NT, bool TOL = false, bool LP = false, int W = 1>
+template <int S, bool NT, bool TOL = false, bool LP = false>
 static void launch_s2d(const StreamArgs &a, int units, bool reduce, hipStream_t s) {
-    const dim3 grid((units + W - 1) / W), block(64 * W);
     if (reduce)
-        hipLaunchKernelGGL((stream_steps2d<S, true, W, NT, TOL, LP>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, true, 1, NT, TOL, LP>), dim3(units), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((stream_steps2d<S, false, W, NT, TOL, LP>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((stream_steps2d<S, false, 1, NT, TOL, LP>), dim3(units), dim3(64), 0, s, a);
 }
 
-template <int S, bool TOL, bool LP, int W = 1>
+template <int S, bool TOL, bool LP>
 static const void *s2d_fn() {
-    return (const void *)&stream_steps2d<S, false, W, false, TOL, LP>;
+    return (const void *)&stream_steps2d<S, false, 1, false, TOL, LP>;
 }
 
 // Launch forms (cfg; one wave per workgroup in all of them -- four-wave
@@ -460,14 +459,9 @@ static const void *s2d_fn() {
 //   planes 2, 5, 6 and the |u| sums in LDS; bitwise S = 6, the default form
 //   at S = 6, where the plain form runs out of registers -- at S = 5 the two
 //   forms measure equal, profiles/r03/ab_forms_s5_s6.log; tolerance S = 6..8).
-//   5, 6: the LP form with 2 / 4 waves per workgroup on adjacent strips of one
-//   segment row (co-scheduled on one CU: the strips' shared overlap columns
-//   are read through its L1 / L2), tolerance S = 6..8.
-// tol: the LBM_FLAG_TOLERANCE collision (collide2t) in forms 0 and 4..6.
-int s2d_form_waves(int cfg) { return cfg == 5 ? 2 : cfg == 6 ? 4 : 1; }
+// tol: the LBM_FLAG_TOLERANCE collision (collide2t) in forms 0 and 4.
 bool s2d_form_ok(int steps, int cfg, bool tol) {
     if (cfg == 4) return steps == 6 || (tol && (steps == 7 || steps == 8));
-    if (cfg == 5 || cfg == 6) return tol && steps >= 6 && steps <= 8;
     if (cfg == 0) return steps >= 2 && steps <= 6;
     if (cfg == 3) return !tol && steps >= 2 && steps <= 6;
     return false;
@@ -478,15 +472,6 @@ bool s2d_form_ok(int steps, int cfg, bool tol) {
 hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
     if (!s2d_form_ok(steps, cfg, tol)) return hipErrorInvalidValue;
     const void *fn = nullptr;
-    if (cfg == 5 || cfg == 6) {
-        const bool w4 = cfg == 6;
-        switch (steps) {
-            case 6: fn = w4 ? s2d_fn<6, true, true, 4>() : s2d_fn<6, true, true, 2>(); break;
-            case 7: fn = w4 ? s2d_fn<7, true, true, 4>() : s2d_fn<7, true, true, 2>(); break;
-            default: fn = w4 ? s2d_fn<8, true, true, 4>() : s2d_fn<8, true, true, 2>(); break;
-        }
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * s2d_form_waves(cfg), 0);
-    }
     if (cfg == 4) {
         switch (steps) {
             case 7: fn = s2d_fn<7, true, true>(); break;
@@ -507,18 +492,6 @@ hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
 
 hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s) {
     if (!s2d_form_ok(steps, cfg, tol)) return hipErrorInvalidValue;
-    if (cfg == 5 || cfg == 6) {
-        switch (steps * 10 + cfg) {
-            case 65: launch_s2d<6, false, true, true, 2>(a, units, reduce, s); break;
-            case 75: launch_s2d<7, false, true, true, 2>(a, units, reduce, s); break;
-            case 85: launch_s2d<8, false, true, true, 2>(a, units, reduce, s); break;
-            case 66: launch_s2d<6, false, true, true, 4>(a, units, reduce, s); break;
-            case 76: launch_s2d<7, false, true, true, 4>(a, units, reduce, s); break;
-            case 86: launch_s2d<8, false, true, true, 4>(a, units, reduce, s); break;
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
     if (cfg == 4) {
         switch (steps * 2 + (tol ? 1 : 0)) {
             case 12: launch_s2d<6, false, false, true>(a, units, reduce, s); break;

@@ -201,29 +201,3 @@ def test_bitwise_stream_rejects_deep_launches(gpu_lib):
     p, obst = load_problem("128x256", iters=8)
     with pytest.raises(gpu_lib.LbmError):
         gpu_lib.Engine(p, obst, kernel=gpu_lib.KERNEL_STREAM, steps_per_launch=7)
-
-
-@pytest.mark.parametrize("cfg", ["5", "6"])
-def test_tolerance_multiwave_forms_equal(gpu_lib, cfg, monkeypatch):
-    """The LP launch forms with 2 / 4 waves per workgroup on adjacent strips
-    (LBM_TOL_CFG 5 / 6) compute the same lattice as the one-wave form, S = 6..8,
-    single domain and 2x2 loop-back (24 steps: fused remainders for S = 7)."""
-    rng = np.random.default_rng(int(cfg))
-    p = lio.Params(600, 260, 24, 10, 0.1, 0.02, 1.7)
-    obst = (rng.random((260, 600)) < 0.03).astype(np.uint8)
-    obst[0, :] = 1
-    cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((260, 600, 9)))).astype(np.float32)
-    out = {}
-    for form in ("4", cfg):
-        monkeypatch.setenv("LBM_DEBUG_KNOBS", "1")
-        monkeypatch.setenv("LBM_TOL_CFG", form)
-        for S in (6, 7, 8):
-            for kw in (dict(), dict(parts=4, grid=(2, 2))):
-                with gpu_lib.Engine(p, obst, devices=[0], **_tol_kw(gpu_lib, steps_per_launch=S, **kw)) as e:
-                    e.load_cells(cells0)
-                    e.run_steps(24, accelerate_first=True)
-                    out[(form, S, len(kw))] = e.store(n_av=24)
-    ref = out[("4", 6, 0)]
-    for key, (cells, av) in out.items():
-        assert np.array_equal(cells, ref[0]), key
-        np.testing.assert_allclose(av, ref[1], rtol=1e-5)
