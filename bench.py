@@ -3,6 +3,16 @@
 
   python bench.py [--gpus N --steps K --warmup W] [--tile 8192x8192]
                   [--kernel auto|stream|step2|vec4|scalar] [--spl S]
+                  [--numerics tolerance|bitwise]
+
+Numerics: `value` is measured with the collision
+--numerics names -- tolerance (default: LBM_FLAG_TOLERANCE, IEEE fp32 with one
+reciprocal of rho per cell, within the tolerance the line states, north_star's
+"within a stated fp32 tolerance") or bitwise (every population identical to
+the reference arithmetic); the other one runs the same workload in aux.
+Steps per launch: the S that finishes K steps soonest by the measured launch
+times (pick_spl; a remainder of >= 2 steps is one fused launch), reported in
+launches.plan.
 
 One "step" = one fused lattice update of every cell (pull-stream, rebound /
 BGK collision, folded acceleration, |u| reduction, halo exchange).
@@ -37,17 +47,18 @@ over ranks.  value = all cells x K / seconds / 1e6 (whole job).
 
 roofline: 72 algorithmic bytes per cell per LAUNCH (9 fp32 loads + 9 fp32
 stores; the 1-byte obstacle mask is excluded) -- a fused launch advances
-steps_per_launch time steps (the default stream kernel: 5) but moves the
-lattice through HBM once -- divided by the average launch duration measured
+steps_per_launch time steps (S = 7 for the tolerance value at K = 20 or 1000)
+but moves the lattice through HBM once -- divided by the average launch duration measured
 with HIP events recorded by the library on the kernel's own stream over the
 timed region (device time of the K steps / launches); peak = 8000 GB/s
 (MI355X HBM3E spec).  traffic = PMC-measured HBM bytes per launch from
 profiles/traffic.json (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) when a
 profile of this workload + kernel exists, else null.  effective_gbs = 72 B x
 cell updates / s (SURVEY 8(d)'s MLUPS x 72 B form), which exceeds the HBM
-peak once temporal blocking pays.  roofline.valu = the bound that binds for
-the fused stream kernel: VALU instructions per launch and the VALU pipe's busy
-fraction from the SQ pass of the same profile (tools/pmc_traffic.py --sq).
+peak once temporal blocking pays.  roofline.valu = VALU instructions per
+launch and the VALU pipe's busy fraction from the SQ pass of the same profile
+(tools/pmc_traffic.py --sq); roofline.bound = "valu" where that pipe is busy
+>= 75 % of the SIMD cycles (the bitwise kernel), else "hbm".
 
 cpu_baseline: the reference's main/LbmCpu.cpp as committed (north_star: "next
 to LbmCpu.cpp timed on the same box's host cores"), built from its source by
@@ -231,7 +242,8 @@ def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
             "reynolds": lio.reynolds_number(p, float(av[-1])), "note": note}
 
 
-def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on: bool, slabs: bool = False) -> dict:
+def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on: bool, slabs: bool = False,
+                     flags: int = 0) -> dict:
     """BASELINE config 4: the fixed 16384x16384 grid (synthetic obstacles) over all
     ranks, RCCL halos overlapped with the interior -- whole-job MLUPS (strong
     scaling; the target is >= 6x at 8 GPUs over 1).  Decomposition: the
@@ -243,7 +255,8 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
     n = 16384
     p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
     obst = synthetic_obstacles(n, n)
-    kw = dict(devices=[local_rank])
+    numerics = "tolerance" if flags & native.FLAG_TOLERANCE else "bitwise"
+    kw = dict(devices=[local_rank], flags=flags, steps_per_launch=pick_spl(steps, 0, numerics))
     if dist_on:
         box = [native.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
@@ -263,6 +276,7 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
             dist.barrier()
         secs = time.perf_counter() - t0
         kernel_used = e.kernel_in_use()
+        spl = e.steps_per_launch()
         rect = e.local_rects()[0]
     if dist_on:
         import torch
@@ -272,7 +286,8 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
     R, C, _ = native.partition(n, n, world, *((world, 1) if slabs else (0, 0)))
     return {"grid": f"{n}x{n}", "steps": steps, "settle_steps": nset,
             "decomposition": f"{R}x{C}" + (" (y slabs)" if slabs else " (reference partitionForIpus rule)"),
-            "sub_domain": f"{rect[2]}x{rect[3]}", "kernel": kernel_used,
+            "sub_domain": f"{rect[2]}x{rect[3]}", "kernel": kernel_used, "numerics": numerics,
+            "launches": launch_plan(steps, spl, kernel_used == "stream"),
             "mlups": round(n * n * steps / secs / 1e6, 1), "ms_per_step": round(secs / steps * 1e3, 4)}
 
 
@@ -683,7 +698,7 @@ def main() -> int:
             aux[f"stream_{other}"] = {"error": str(exc)}
     if n > 1 and not args.no_aux:
         try:
-            ms = measure_weak(tnx, tny, n, 1, args, kernel, kflags, rank, world, local_rank, dist_on)
+            ms = measure_weak(tnx, tny, n, 1, args, kernel, kflags_main, rank, world, local_rank, dist_on)
             aux["weak_slabs"] = {"decomposition": f"{n}x1 (y slabs)", "global_grid": f"{ms['nx']}x{ms['ny']}",
                                  "mlups": round(ms["nx"] * ms["ny"] * args.steps / ms["elapsed"] / 1e6, 1),
                                  "ms_per_step": round(ms["elapsed"] / args.steps * 1e3, 5), "kernel": ms["kernel"]}
@@ -694,7 +709,8 @@ def main() -> int:
             if slabs and n == 1:
                 continue
             try:
-                aux[key] = aux_strong_16384(100, rank, world, local_rank, dist_on, slabs=slabs)
+                aux[key] = aux_strong_16384(100, rank, world, local_rank, dist_on, slabs=slabs,
+                                            flags=kflags_main & native.FLAG_TOLERANCE)
             except Exception as exc:
                 aux[key] = {"error": str(exc)}
     if not args.no_aux and not args.no_d3q19:

@@ -706,7 +706,7 @@ struct lbm3d_handle {
     bool nt = true;    // LBM3D_NT: non-temporal output stores
     bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two), single slab or z slabs
     int seg = 64;      // LBM3D_SEG: z planes per block of the two-step kernel (32-128 equal within noise at 512^3)
-    int th = 12;       // LBM3D_TH: rows (waves) per block of the two-step kernel (12, 14, 15)
+    int th = 12;       // LBM3D_TH: rows (waves) per block of the two-step kernel (12 only since round 3)
     bool skip = false; // LBM3D_SKIP: waves skip the collisions of rows no later level reads (not faster)
     // LBM3D_PD: input planes in flight in the two-step kernel -- 0 (default): the
     // next plane loaded once level 1 has consumed the current one (44.7 vs
@@ -912,16 +912,12 @@ struct lbm3d_handle {
         if (s.nzs > 4) r.push_back({2, s.nzs - 2});
         return r;
     }
-    // switch key of the instantiated step3d_two<TH, SKIP, PD> variants, -1 if none
+    // switch key of the instantiated step3d_two<TH, SKIP, PD> variants, -1 if none:
+    // 12 rows without skip, late load (default) or one plane prefetched.  Blocks
+    // of 14-16 rows, the row skip and two prefetched planes were measured and
+    // removed (profiles/r02/d3q19/ab_two_th_skip_pd.log, profiles/r03/d3q19/ab_pd.log).
     static int two_variant(int th, bool skip, int pd) {
-        if ((th != 12 && th != 14 && th != 15 && th != 16) || pd < 0 || pd > 2) return -1;
-        if (pd == 0) return (th == 12 || th == 16) && !skip ? 100 + th : -1;  // late-load variants
-        const int key = (th * 2 + (skip ? 1 : 0)) * 2 + (pd - 1);
-        switch (key) {
-            case 48: case 49: case 50: case 51: case 56: case 58: case 59: case 60: case 62: case 63: case 64:
-                return key;
-            default: return -1;
-        }
+        return (th == 12 && !skip && (pd == 0 || pd == 1)) ? pd : -1;
     }
     int two_blocks(int z0, int zn) const {
         return ((p.nx + T3OX - 1) / T3OX) * ((p.ny + th - 5) / (th - 4)) * ((zn - z0 + seg - 1) / seg);
@@ -968,19 +964,8 @@ struct lbm3d_handle {
             return;
         }
         switch (two_variant(th, skip, pd)) {
-            case 48: hipLaunchKernelGGL((step3d_two<12, false, 1>), g, b, 0, st, a); break;
-            case 49: hipLaunchKernelGGL((step3d_two<12, false, 2>), g, b, 0, st, a); break;
-            case 50: hipLaunchKernelGGL((step3d_two<12, true, 1>), g, b, 0, st, a); break;
-            case 51: hipLaunchKernelGGL((step3d_two<12, true, 2>), g, b, 0, st, a); break;
-            case 56: hipLaunchKernelGGL((step3d_two<14, false, 1>), g, b, 0, st, a); break;
-            case 58: hipLaunchKernelGGL((step3d_two<14, true, 1>), g, b, 0, st, a); break;
-            case 59: hipLaunchKernelGGL((step3d_two<14, true, 2>), g, b, 0, st, a); break;
-            case 60: hipLaunchKernelGGL((step3d_two<15, false, 1>), g, b, 0, st, a); break;
-            case 62: hipLaunchKernelGGL((step3d_two<15, true, 1>), g, b, 0, st, a); break;
-            case 63: hipLaunchKernelGGL((step3d_two<15, true, 2>), g, b, 0, st, a); break;
-            case 64: hipLaunchKernelGGL((step3d_two<16, false, 1>), g, b, 0, st, a); break;
-            case 112: hipLaunchKernelGGL((step3d_two<12, false, 0>), g, b, 0, st, a); break;
-            case 116: hipLaunchKernelGGL((step3d_two<16, false, 0>), g, b, 0, st, a); break;
+            case 0: hipLaunchKernelGGL((step3d_two<12, false, 0>), g, b, 0, st, a); break;
+            case 1: hipLaunchKernelGGL((step3d_two<12, false, 1>), g, b, 0, st, a); break;
             default: throw fail3(LBM_E_INTERNAL, "unvalidated two-step variant");
         }
         H3(hipGetLastError());

@@ -238,14 +238,12 @@ def test_d3q19_rccl_two_step_self_exchange_bitwise(gpu_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("th,skip,pd", [("12", "0", "1"), ("12", "1", "1"), ("14", "1", "1"), ("15", "1", "1"), ("15", "0", "1"),
-                                         ("12", "1", "2"), ("15", "1", "2"), ("16", "0", "1"), ("16", "0", "0"),
-                                         ("12", "0", "0")])
+@pytest.mark.parametrize("th,skip,pd", [("12", "0", "0"), ("12", "0", "1")])
 @pytest.mark.parametrize("nx,ny,nz,parts", [(64, 8, 5, 1), (125, 23, 9, 1), (61, 17, 3, 1), (70, 31, 24, 3)])
 def test_d3q19_two_step_block_rows_bitwise(gpu_lib, nx, ny, nz, parts, th, skip, pd, monkeypatch):
-    """The two-step kernel's block heights (LBM3D_TH: 12, 14, 15, 16 rows =
-    waves, up to 115 KB of LDS) with and without the wave-uniform skip of the rows no
-    later level reads (LBM3D_SKIP): bitwise vs the oracle on partial and
+    """The two-step kernel's two load schedules (LBM3D_PD 0: the next plane
+    loaded once level 1 is done with the current one, the default; 1: one plane
+    prefetched a whole iteration ahead): bitwise vs the oracle on partial and
     wrapped tiles (ny below and above one block's owned rows), one slab and
     z slabs, 9 steps (four passes + one one-step launch)."""
     monkeypatch.setenv("LBM3D_TH", th)
