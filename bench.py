@@ -553,6 +553,31 @@ class AuxWatchdog:
         self._print(self.out)
 
 
+MAIN_WATCHDOG_EXIT = 4
+
+
+def main_watchdog(budget_s: float, rank: int, n: int) -> threading.Timer | None:
+    """N > 1: bounds the multi-rank check and the timed measurement (RCCL
+    between real devices runs for the first time on the driver's multi-GPU
+    node).  Past the budget rank 0 prints a line that says so and every rank
+    exits with MAIN_WATCHDOG_EXIT (4), so a hung exchange frees the node
+    instead of holding it until the launcher's limit."""
+    if budget_s <= 0 or n <= 1:
+        return None
+
+    def fire():
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "MLUPS", "n_gpus": n,
+                              "error": f"multi-rank check / timed measurement exceeded {budget_s:.0f} s"}), flush=True)
+        log(f"main watchdog: {budget_s:.0f} s exceeded, exiting with status {MAIN_WATCHDOG_EXIT}")
+        os._exit(MAIN_WATCHDOG_EXIT)
+
+    t = threading.Timer(budget_s, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -576,6 +601,8 @@ def main() -> int:
     ap.add_argument("--no-d3q19", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="skip the 16384^2 strong-scaling aux (config 4)")
     ap.add_argument("--d3q19-n", type=int, default=512, help="D3Q19 aux grid edge (BASELINE config 5: 512)")
+    ap.add_argument("--main-budget", type=float, default=600.0,
+                    help="N > 1: seconds the multi-rank check plus the timed measurement may take (0: no limit)")
     ap.add_argument("--aux-budget", type=float, default=300.0,
                     help="seconds the aux measurements may take after the main one; past it rank 0 prints the "
                          "line with the aux done so far and every rank exits (0: no limit)")
@@ -602,6 +629,7 @@ def main() -> int:
 
     tnx, tny = (int(v) for v in args.tile.lower().split("x"))
     R, C = weak_grid(n, tnx, tny)
+    mwd = main_watchdog(args.main_budget, rank, n)
     mrc = None
     if dist_on:
         try:
@@ -614,6 +642,8 @@ def main() -> int:
     m = measure_weak(tnx, tny, R, C, args, kernel, kflags_main, rank, world, local_rank, dist_on)
     nx, ny, elapsed, dev_secs = m["nx"], m["ny"], m["elapsed"], m["dev_secs"]
     kernel_used, steps_per_launch = m["kernel"], m["spl"]
+    if mwd is not None:
+        mwd.cancel()
 
     total_cells = nx * ny
     value = total_cells * args.steps / elapsed / 1e6

@@ -50,3 +50,28 @@ def test_watchdog_finish_prints_once():
     assert p.returncode == 0
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert lines == [json.dumps({"metric": "m", "value": 2.0, "aux": {"x": 1}})]
+
+
+def test_main_watchdog_multi_rank_hang():
+    """N > 1: a hung multi-rank check / timed measurement ends every rank with
+    status 4; rank 0 prints a line naming the failure (no value)."""
+    p, dt = run('w = bench.main_watchdog(0.5, 0, 8)\n'
+                'time.sleep(30)\n')
+    assert p.returncode == bench_exit("MAIN_WATCHDOG_EXIT") == 4, p.stderr
+    d = json.loads(p.stdout.strip())
+    assert d["value"] is None and d["n_gpus"] == 8 and "exceeded" in d["error"]
+    assert dt < 20
+    p, _ = run('w = bench.main_watchdog(0.5, 5, 8)\ntime.sleep(30)\n')
+    assert p.returncode == 4 and p.stdout.strip() == ""
+
+
+def test_main_watchdog_off_for_one_gpu_and_cancellable():
+    p, _ = run('assert bench.main_watchdog(0.5, 0, 1) is None\n'
+               'w = bench.main_watchdog(0.5, 0, 2); w.cancel(); time.sleep(1.0); print("ok")\n')
+    assert p.returncode == 0 and p.stdout.strip() == "ok"
+
+
+def bench_exit(name: str) -> int:
+    sys.path[:0] = [str(ROOT), str(ROOT / "lbm-graphcore_amd")]
+    import bench
+    return getattr(bench, name)
