@@ -27,6 +27,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "lbm3d_hip.h"
@@ -715,6 +716,9 @@ struct lbm3d_handle {
     long long kspad = 0;  // LBM3D_KSPAD: floats appended to each speed plane (multiple of 64)
     const char *lattice_pad = nullptr;  // LBM_LATTICE_PAD (debug knob)
     bool poison = false;  // LBM_POISON=1: fresh allocations filled with NaN bytes
+    int probe_tries = 4;  // LBM3D_PLACEMENT_TRIES: lattice pairs the placement probe times (1 = off)
+    long long probe_min_cells = 1LL << 26;  // LBM3D_PROBE_MIN_CELLS: smallest single slab probed
+    bool probe_log = false;  // LBM_PLACEMENT_LOG: print the probe's per-pair times
     bool tolerance = false;  // LBM_FLAG_TOLERANCE: the two-step passes use cell3dt (not bitwise)
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
@@ -768,6 +772,9 @@ struct lbm3d_handle {
         if (const char *d = knob("LBM3D_PD")) pd = atoi(d);
         if (const char *k = knob("LBM3D_KSPAD")) kspad = (std::max(0LL, atoll(k)) + 63) / 64 * 64;
         lattice_pad = knob("LBM_LATTICE_PAD");
+        if (const char *t = knob("LBM3D_PLACEMENT_TRIES")) probe_tries = std::max(1, atoi(t));
+        if (const char *m = knob("LBM3D_PROBE_MIN_CELLS")) probe_min_cells = std::max(0LL, atoll(m));
+        probe_log = knob("LBM_PLACEMENT_LOG") != nullptr;
         if (tolerance) {  // the tolerance pass exists for the default block only
             th = 12;
             skip = false;
@@ -835,6 +842,102 @@ struct lbm3d_handle {
         H3(hipSetDevice(slabs[0].dev));
         H3(hipEventCreate(&t0));
         H3(hipEventCreate(&t1));
+        placement_probe();
+    }
+
+    // Placement probe (the D3Q19 counterpart of lbm_engine.hip's; DESIGN.md
+    // §4.9): the two-step pass runs at an engine-to-engine spread of about
+    // +-5 % at 512^3 fixed by where the lattices land (39.9-44.2 GLUPS over
+    // six engines in one process, profiles/r03/d3q19/spread.log).  A single
+    // slab of at least 2^26 cells allocates up to probe_tries lattice pairs
+    // (at most 96 GB held at once: four at 512^3), times two-step passes on
+    // each (constant populations; one warm-up round, then the best of two
+    // interleaved rounds), keeps the fastest pair and frees the rest; the kept
+    // pair is filled as a fresh allocation is, so the engine's state is as if
+    // the probe had not run.  Failures inside free every extra candidate and
+    // restore the original pair.
+    void placement_probe() {
+        if (multi() || !use_two() || slabs.size() != 1) return;
+        Slab &s = slabs[0];
+        if ((long long)p.nx * p.ny * p.nz < probe_min_cells || s.f_joint) return;
+        const size_t floats = (size_t)(s.nzs + 4) * PL;
+        const size_t pair_bytes = 2 * sizeof(float) * floats;
+        const int cap = (int)std::max<size_t>(1, (96ull << 30) / pair_bytes);
+        const int tries = std::min({probe_tries, 8, cap});
+        if (tries <= 1) return;
+        H3(hipSetDevice(s.dev));
+        std::vector<std::array<float *, 2>> cand{{s.f[0], s.f[1]}};
+        size_t keep = 0;
+        auto set_pair = [&](size_t c) {
+            for (int k = 0; k < 2; ++k) {
+                s.f[k] = cand[c][k];
+                s.o[k] = s.f[k] + 2 * PL;
+            }
+            s.cur = 0;
+        };
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        try {
+            for (int c = 1; c < tries; ++c) {
+                std::array<float *, 2> f{nullptr, nullptr};
+                if (hipMalloc(&f[0], sizeof(float) * floats) != hipSuccess) { (void)hipGetLastError(); break; }
+                if (hipMalloc(&f[1], sizeof(float) * floats) != hipSuccess) {
+                    (void)hipGetLastError();
+                    (void)hipFree(f[0]);
+                    break;
+                }
+                cand.push_back(f);
+            }
+            for (auto &f : cand)  // 0.05f everywhere: rho = 0.95, no tiny-density path
+                for (float *q : f) H3(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(q), 0x3d4ccccd, floats, s.s_comp));
+            H3(hipEventCreate(&e0));
+            H3(hipEventCreate(&e1));
+            std::vector<float> best(cand.size(), 1e30f);
+            for (int round = 0; round < 3; ++round)
+                for (size_t c = 0; c < cand.size(); ++c) {
+                    set_pair(c);
+                    H3(hipEventRecord(e0, s.s_comp));
+                    for (int i = 0; i < 2; ++i) {
+                        launch_two(s, 0, s.nzs, 0, s.s_comp);
+                        s.cur ^= 1;
+                    }
+                    H3(hipEventRecord(e1, s.s_comp));
+                    H3(hipEventSynchronize(e1));
+                    float ms = 0.f;
+                    H3(hipEventElapsedTime(&ms, e0, e1));
+                    if (round > 0) best[c] = std::min(best[c], ms / 2);  // round 0: clock warm-up
+                }
+            for (size_t c = 1; c < cand.size(); ++c)
+                if (best[c] < best[keep]) keep = c;
+            if (probe_log) {
+                fprintf(stderr, "lbm3d placement probe (%dx%dx%d): ms per two-step pass", p.nx, p.ny, p.nz);
+                for (float v : best) fprintf(stderr, " %.4f", v);
+                fprintf(stderr, "; kept pair %zu\n", keep);
+            }
+            for (size_t c = 0; c < cand.size(); ++c)
+                if (c != keep)
+                    for (float *&q : cand[c]) {
+                        (void)hipFree(q);
+                        q = nullptr;
+                    }
+            set_pair(keep);
+            for (float *q : s.f) fill_fresh(q, sizeof(float) * floats, s.s_comp);
+            H3(hipEventDestroy(e0));
+            H3(hipEventDestroy(e1));
+        } catch (...) {
+            // the handle keeps exactly one pair: the original while it exists, else the kept one
+            const size_t own = cand[0][0] ? 0 : keep;
+            for (size_t c = 0; c < cand.size(); ++c)
+                if (c != own)
+                    for (float *&q : cand[c])
+                        if (q) {
+                            (void)hipFree(q);
+                            q = nullptr;
+                        }
+            set_pair(own);
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+            throw;
+        }
     }
 
     int blocks_for(int planes) const {

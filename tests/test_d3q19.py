@@ -293,3 +293,22 @@ def test_d3q19_tolerance_vs_oracle(gpu_lib, parts):
     assert not np.array_equal(cells, ref)  # the flag really selects the other collision
     assert np.array_equal(cells, one)
     np.testing.assert_allclose(av, ref_av, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, 4])
+def test_d3q19_placement_probe_transparent(gpu_lib, flags, monkeypatch):
+    """The D3Q19 placement probe (forced on a small slab: LBM3D_PROBE_MIN_CELLS=0,
+    three candidate pairs) leaves the engine as a fresh one: bitwise the same
+    lattice and av_vels as with the probe off, and (bitwise mode) as the oracle."""
+    p, obst, c0 = _problem(70, 31, 24, 5)
+    out = []
+    for tries in ("1", "3"):
+        monkeypatch.setenv("LBM3D_PLACEMENT_TRIES", tries)
+        monkeypatch.setenv("LBM3D_PROBE_MIN_CELLS", "0")
+        out.append(_gpu3d(gpu_lib, p, obst, c0, 9, devices=[0], flags=flags))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    if flags == 0:
+        ref, _ = oracle.run3d(p, obst, 9, c0)
+        assert np.array_equal(out[1][0], ref)

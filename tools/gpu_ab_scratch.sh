@@ -1,6 +1,5 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
-V="--variant lp:FLAGS=4 --variant lpnt:FLAGS=4,LBM_TOL_CFG=7"
 bash tools/gpu_steps.sh \
-  "400|ab_nt|python3 tools/ab_bench.py --n 8192 --steps 98 --warmup 14 --rounds 4 --check $V" \
-  "300|ab_nt20|python3 tools/ab_bench.py --n 8192 --steps 20 --warmup 5 --rounds 4 $V"
-cat gpurun_out/ab_nt.log gpurun_out/ab_nt20.log | grep variant
+  "300|t_probe3d|python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_d3q19.py -k 'probe or slab'" \
+  "400|d3spread|LBM_DEBUG_KNOBS=1 LBM_PLACEMENT_LOG=1 python3 tools/d3_spread.py --engines 6"
+grep -h "passed\|failed" gpurun_out/t_probe3d.log | tail -2; cat gpurun_out/d3spread.log | grep "engine\|probe"
