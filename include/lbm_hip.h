@@ -58,8 +58,8 @@ enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
  * that are multiples of 4).  STEP2: fused two-step launches through LDS.
  * STREAM: fused S-step launches (S = steps_per_launch, 2..6, 2..8 with
  * LBM_FLAG_TOLERANCE; default 6, 7 with it) streaming rows through registers; a run of
- * K steps on one sub-domain is K / S launches plus, when 2 <= K % S, one
- * fused launch of K % S steps (else K % S one-step launches).  RESIDENT: every step of a run in one persistent
+ * K steps is K / S launches plus, when 2 <= K % S, one fused launch of K % S
+ * steps (else K % S one-step launches), single and decomposed domains alike.  RESIDENT: every step of a run in one persistent
  * launch with the lattice held on chip (LDS + registers) -- single
  * sub-domain grids small enough for all of their 64-column tiles to be
  * co-resident (1024x1024 and below on MI355X).  PIPELINE: the unfused
