@@ -23,7 +23,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int NX = 8192, NY = 8192, S = 4, Q = 9;
-constexpr int XOFF = 64, GR = 4;
+constexpr int XOFF = 64, GR = 8;  // GR ghost rows each side: >= every SS used below
 constexpr int RF = ((NX + XOFF + GR + 2 + 63) / 64) * 64;  // floats per plane row
 constexpr long long PITCH = (long long)Q * RF;             // floats per lattice row
 
@@ -45,8 +45,12 @@ struct Vec<4> { typedef f4 T; };
 // 2: f[y][x/128][k][x%128] (row-interleaved blocks of 128 columns: one row of a
 // 128-column block = 9 x 512 B contiguous).
 // W waves per workgroup take W adjacent strips (co-scheduled on one CU).
-// NT: non-temporal stores.
-template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1, bool STORE = true>
+// NT: non-temporal stores.  SS: steps (re-streamed rows and overlap columns).
+// ALT: units of odd segments walk their rows top-down, so two neighbouring
+// segments read their shared 2*SS boundary rows at about the same time (both
+// at the start or both at the end of the unit) instead of a unit apart.
+template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1, bool STORE = true, int SS = S,
+          bool ALT = false>
 __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin, float *__restrict__ fout, int hs,
                                                   int nstrip, int total, float *sink) {
     typedef typename Vec<V>::T T;
@@ -55,10 +59,10 @@ __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin,
     const int t = xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6);
     if (t >= total) return;
     const int lane = threadIdx.x & 63;
-    const int ow = 64 * V - 2 * S;
+    const int ow = 64 * V - 2 * SS;
     const int seg = t / nstrip, strip = t - seg * nstrip;
     const int xo0 = strip * ow, xo1 = min(xo0 + ow, NX);
-    const int base = ((xo0 - S) & ~(V - 1));
+    const int base = ((xo0 - SS) & ~(V - 1));
     const int xa = base + V * lane;
     const bool own = xa >= xo0 && xa + V - 1 < xo1;
     const int yo0 = seg * hs, yo1 = min(yo0 + hs, NY);
@@ -69,17 +73,22 @@ __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin,
     extern __shared__ float occupancy_limiter[];
     if (hs < 0) occupancy_limiter[threadIdx.x] = 0.f;  // never: keeps the dynamic LDS request
     T v[Q], nv[Q], nv2[Q];
-    int j = yo0 - S;
-    const int jl = yo1 + S - 1;
+    const bool down = ALT && (seg & 1);
+    const int d = down ? -1 : 1;
+    const int jf = down ? yo1 + SS - 1 : yo0 - SS;  // first and last row of the walk
+    const int jl = down ? yo0 - SS : yo1 + SS - 1;
+    auto clampj = [&](int jj) { return down ? max(jj, jl) : min(jj, jl); };
+    int j = jf;
 #pragma unroll
     for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const T *>(src + (long long)j * PS + (long long)k * KS);
     if (PD == 2) {
 #pragma unroll
-        for (int k = 0; k < Q; ++k) nv2[k] = *reinterpret_cast<const T *>(src + (long long)min(j + 1, jl) * PS + (long long)k * KS);
+        for (int k = 0; k < Q; ++k) nv2[k] = *reinterpret_cast<const T *>(src + (long long)clampj(j + d) * PS + (long long)k * KS);
     }
     f2 acc[4] = {f2{0.f, 0.f}, f2{1.f, 1.f}, f2{2.f, 2.f}, f2{3.f, 3.f}};
-    for (; j <= jl; ++j) {
-        const int jn = min(j + PD, jl);
+    const int nrows = yo1 - yo0 + 2 * SS;
+    for (int i = 0; i < nrows; ++i, j += d) {
+        const int jn = clampj(j + PD * d);
         if (PD == 2) {
 #pragma unroll
             for (int k = 0; k < Q; ++k) nv[k] = nv2[k];
@@ -89,8 +98,8 @@ __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin,
         // stand-in arithmetic: WORK independent packed FMAs per lane
 #pragma unroll
         for (int w = 0; w < WORK; ++w) acc[w & 3] = __builtin_elementwise_fma(acc[w & 3], f2{1.0001f, 0.9999f}, f2{v[w % Q][0], v[(w + 1) % Q][1]});
-        const int y = j - S;
-        if (STORE && y >= yo0 && own) {
+        const int y = j - SS * d;
+        if (STORE && y >= yo0 && y < yo1 && own) {
 #pragma unroll
             for (int k = 0; k < Q; ++k) {
                 T o = v[k];
@@ -108,23 +117,24 @@ __global__ __launch_bounds__(64 * W) void pattern(const float *__restrict__ fin,
     if (acc[0][0] == 12345.f) sink[0] = acc[1][1] + acc[2][0] + acc[3][1];
 }
 
-template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1, bool STORE = true>
+template <int V, int WORK, int LAYOUT = 0, int W = 1, bool NT = false, int PD = 1, bool STORE = true, int SS = S,
+          bool ALT = false>
 void run(const char *name, float *a, float *b, int hs, float *sink, int waves_per_simd = 0) {
     // waves_per_simd > 0: dynamic LDS so that only that many waves fit per SIMD
     const size_t lds = waves_per_simd > 0 ? (size_t)(160 * 1024) / (4 * waves_per_simd) * W - 256 : 0;
-    const int ow = 64 * V - 2 * S;
+    const int ow = 64 * V - 2 * SS;
     const int nstrip = (NX + ow - 1) / ow, nseg = (NY + hs - 1) / hs, total = nstrip * nseg;
     const int blocks = (total + W - 1) / W;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (int i = 0; i < 20; ++i)
-        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD, STORE>), dim3(blocks), dim3(64 * W), lds, 0, a, b, hs, nstrip, total,
+        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD, STORE, SS, ALT>), dim3(blocks), dim3(64 * W), lds, 0, a, b, hs, nstrip, total,
                            sink);
     const int reps = 40;
     (void)hipEventRecord(e0);
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD, STORE>), dim3(blocks), dim3(64 * W), lds, 0, (i & 1) ? b : a,
+        hipLaunchKernelGGL((pattern<V, WORK, LAYOUT, W, NT, PD, STORE, SS, ALT>), dim3(blocks), dim3(64 * W), lds, 0, (i & 1) ? b : a,
                            (i & 1) ? a : b, hs, nstrip, total, sink);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
@@ -132,7 +142,7 @@ void run(const char *name, float *a, float *b, int hs, float *sink, int waves_pe
     (void)hipEventElapsedTime(&ms, e0, e1);
     ms /= reps;
     const double lattice = 72.0 * NX * NY;                                      // algorithmic bytes per pass
-    const double moved = 36.0 * NX * NY * ((double)(hs + 2 * S) / hs) * (64.0 * V / ow) + 36.0 * NX * NY;
+    const double moved = 36.0 * NX * NY * ((double)(hs + 2 * SS) / hs) * (64.0 * V / ow) + 36.0 * NX * NY;
     printf("{\"variant\": \"%s\", \"V\": %d, \"hs\": %d, \"work\": %d, \"waves\": %d, \"waves_per_simd\": %d, "
            "\"ms\": %.4f, \"lattice_TBps\": %.3f, \"moved_TBps\": %.3f, \"err\": \"%s\"}\n",
            name, V, hs, WORK, total, waves_per_simd, ms, lattice / ms / 1e9, moved / ms / 1e9,
@@ -205,6 +215,17 @@ int main(int argc, char **argv) {
         run<4, 0, 0>("V4_hs96_o8", a, b, 96, sink, 0);
         run<2, 0, 0>("L0_hs400_o8", a, b, 400, sink, 0);
         run<2, 0, 0>("L0_hs20_o8", a, b, 20, sink, 0);
+    } else if (which == 3) {
+        // S = 7, 144-row segments (the tolerance default): odd segments walking
+        // down (ALT) against all up; with and without stand-in arithmetic
+        for (int rep = 0; rep < 2; ++rep) {
+            run<2, 0, 0, 1, false, 1, true, 7, false>("s7_hs144_up", a, b, 144, sink, 2);
+            run<2, 0, 0, 1, false, 1, true, 7, true>("s7_hs144_alt", a, b, 144, sink, 2);
+            run<2, 0, 0, 1, false, 1, true, 7, false>("s7_hs48_up", a, b, 48, sink, 2);
+            run<2, 0, 0, 1, false, 1, true, 7, true>("s7_hs48_alt", a, b, 48, sink, 2);
+            run<2, 384, 0, 1, false, 1, true, 7, false>("s7_hs144_up_work384", a, b, 144, sink, 2);
+            run<2, 384, 0, 1, false, 1, true, 7, true>("s7_hs144_alt_work384", a, b, 144, sink, 2);
+        }
     } else {
         // layouts: row-interleaved (0), planar (1), 128-column blocks (2); hs 35 and 96
         run<2, 0, 0>("L0_hs35_o2", a, b, 35, sink, 2);
