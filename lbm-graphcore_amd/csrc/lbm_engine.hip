@@ -1701,7 +1701,8 @@ struct lbm_handle {
         // shorter launch's halo cells in the innermost rem ghost columns / rows
         // (send-buffer positions), where the periodic / neighbour images of
         // its cells belong, so the exchange of this launch leaves the rem-deep
-        // ring right and refresh_halos below restores the whole spl-deep ring
+        // ring right; the next run starts by restoring the whole spl-deep ring
+        // (ring_stale)
         const bool fused_rem = fused && use_stream && rem >= 2;
         if (fused_rem) launch_once(true, rem);
         for (int i = 0; i < (fused_rem ? 0 : rem); ++i) launch_once(false);  // remainder: one-step kernel (W1 halo) ...
