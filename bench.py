@@ -402,12 +402,12 @@ def multi_rank_check(rank: int, world: int, local_rank: int, n: int = 2048) -> d
     return {"passed": bool(ok[0]), "grid": f"{n}x{n}", "cases": results}
 
 
-# Device ms per fused launch of S steps at 8192^2 (profiles/r03/deep_tol/,
-# profiles/r03/ab_forms_s5_s6.log): bitwise and tolerance collision; a launch
-# of 2..4 steps is bound by the lattice pass (~1.2 ms); a one-step (vec4)
+# Device ms per fused launch of S steps at 8192^2 (profiles/r03/ab_spl_ow16.log,
+# 16-column aligned strips): bitwise and tolerance collision; a launch of
+# 2..5 steps is bound by the lattice pass (~1.1 ms); a one-step (vec4)
 # launch 0.81 ms.
-LAUNCH_MS = {"bitwise": {2: 1.15, 3: 1.18, 4: 1.2, 5: 1.24, 6: 1.43},
-             "tolerance": {2: 1.15, 3: 1.18, 4: 1.2, 5: 1.21, 6: 1.2, 7: 1.22, 8: 1.47}}
+LAUNCH_MS = {"bitwise": {2: 1.12, 3: 1.07, 4: 1.10, 5: 1.18, 6: 1.39},
+             "tolerance": {2: 1.11, 3: 1.07, 4: 1.08, 5: 1.10, 6: 1.10, 7: 1.13, 8: 1.52}}
 ONE_STEP_MS = 0.81
 
 

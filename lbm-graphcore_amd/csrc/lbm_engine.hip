@@ -684,13 +684,23 @@ struct lbm_handle {
         // owned columns per strip: 64 - 2S (one column per lane); 128 - 2S
         // (two per lane), 2 fewer when the strip's first cell minus S is odd
         // (float2 alignment shifts the wave one column left)
-        auto ow_of = [&](int rx) { return ((rx - S) & 1) ? 126 - 2 * S : 128 - 2 * S; };
+        // ow16: owned widths (and the x bands) rounded down to 16 columns, so
+        // that with 64-B aligned interior rows every strip's stores start and
+        // end on a 64-B sector -- partial-sector stores cost more than the
+        // extra recomputed columns (8192^2: tolerance S = 4 / 6 +6 / +8 %,
+        // bitwise S = 5 +6 %; bitwise S = 6, VALU-bound, -4 % and keeps the
+        // natural width; profiles/r03/ab_ow16.log)
+        const bool ow16 = knob("LBM_STREAM_OW16", (tolerance || S <= 5) ? 1 : 0) != 0;
+        auto ow_of = [&](int rx) {
+            const int n = ((rx - S) & 1) ? 126 - 2 * S : 128 - 2 * S;
+            return ow16 ? n / 16 * 16 : n;
+        };
         const bool xdec = s.remote[DE] || s.remote[DW];
         const bool ydec = s.remote[DN] || s.remote[DS];
         // a decomposed x side's boundary band is one whole strip wide when the
         // sub-domain has room: an S-column band costs nearly a full strip per
         // segment for S useful columns (tools/ab_parts.py)
-        const int ow_min = 126 - 2 * S;
+        const int ow_min = ow16 ? (126 - 2 * S) / 16 * 16 : 126 - 2 * S;
         const int xb = (xdec && s.w >= 4 * ow_min) ? ow_min : b;
         const int y0 = ydec ? b : 0, y1 = ydec ? s.h - b : s.h;
         const int x0 = xdec ? xb : 0, x1 = xdec ? s.w - xb : s.w;

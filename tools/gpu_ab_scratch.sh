@@ -1,3 +1,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
-bash tools/gpu_steps.sh "500|d3spread|LBM_DEBUG_KNOBS=1 LBM_PLACEMENT_LOG=1 python3 tools/d3_spread.py --engines 5"
-cat gpurun_out/d3spread.log | grep "engine\|probe"
+K="LBM_DEBUG_KNOBS=1"
+V=""
+for s in 2 3 4 5 6 7 8; do V="$V --variant t$s:FLAGS=4,$K,LBM_TOL_S=$s"; done
+for s in 2 3 4 5 6; do V="$V --variant b$s:$K,LBM_STREAM_S=$s"; done
+bash tools/gpu_steps.sh "500|ab_spl_ow16|python3 tools/ab_bench.py --n 8192 --steps 840 --warmup 24 --rounds 2 $V"
+grep variant gpurun_out/ab_spl_ow16.log | cut -c1-20,110-230
