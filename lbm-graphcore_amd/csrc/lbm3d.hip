@@ -437,7 +437,7 @@ struct T3 {
 struct Two3Args {
     const float *fin;   // origin of the lattice read (ghost planes -2, -1, nz, nz + 1 filled)
     float *fout;
-    const uint8_t *obst;  // plane 0 of [nz + 4][ny][nx]: two planes of neighbour / periodic images each side
+    const uint8_t *obst;  // plane 0 of [nz + 6][ny][nx]: three planes of neighbour / periodic images each side
     long long PL, KS;
     int px, nx, ny, nz, seg;
     int z0, zn;           // output planes [z0, zn) of this launch, in segments of seg planes
@@ -608,6 +608,101 @@ __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// step3d_three: three time steps per pass (single slab).  The same 64 x 12
+// block and level3 building block with a third level: level 1 computes plane
+// j-1 at t+1, level 2 plane j-2 at t+2, level 3 plane j-3 at t+3 as input
+// plane j arrives.  A three-cell ring in x and y is recomputed: owned 58 x 6
+// of 64 x 12 loaded cells, three levels of 14 plane slots = 126 KB of LDS (one
+// block per CU, three waves per SIMD).  Algorithmic traffic per cell update:
+// (19 x 768 loads + 19 x 348 stores) x 4 B / (3 x 348) = 81.2 B instead of
+// 98.8 for two steps per pass (152 for one).  Input planes zs-3 .. ze+2: the
+// lattice carries three ghost planes each side (GZ3), refreshed from the
+// periodic images before every pass.  Same cell3d / cell3dt arithmetic as the
+// other passes: bitwise equal to them (and the oracle) in bitwise mode.
+constexpr int T3OX3 = T3W - 6;  // owned columns
+constexpr int T3TH3 = 12;       // rows (waves) per block
+constexpr int T3OY3 = T3TH3 - 6;
+constexpr int GZ3 = 3;  // ghost planes each side of every slab lattice (and obst_g)
+
+template <bool TOL>
+__global__ __launch_bounds__(T3W *T3TH3) void step3d_three(Two3Args a) {
+    __shared__ float lds1[T3<T3TH3>::LDS], lds2[T3<T3TH3>::LDS], lds3[T3<T3TH3>::LDS];
+    __shared__ float red[3][T3TH3];
+    const int lane = threadIdx.x, wy = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int ox = blockIdx.x * T3OX3, oy = blockIdx.y * T3OY3;
+    const int x = (((ox - 3 + lane) % a.nx) + a.nx) % a.nx;
+    const int y = (((oy - 3 + wy) % a.ny) + a.ny) % a.ny;
+    const bool own = lane >= 3 && lane < T3W - 3 && wy >= 3 && wy < T3TH3 - 3 && ox + lane - 3 < a.nx &&
+                     oy + wy - 3 < a.ny;
+    const int zs = a.z0 + blockIdx.z * a.seg, ze = min(zs + a.seg, a.zn);
+    const long long row = (long long)y * a.px + x;
+    float r0a[3] = {0.f, 0.f, 0.f}, r9aa[3] = {0.f, 0.f, 0.f}, r9ba[3] = {0.f, 0.f, 0.f};
+    float r0b[3] = {0.f, 0.f, 0.f}, r9ab[3] = {0.f, 0.f, 0.f}, r9bb[3] = {0.f, 0.f, 0.f};
+    float r0c[3] = {0.f, 0.f, 0.f}, r9ac[3] = {0.f, 0.f, 0.f}, r9bc[3] = {0.f, 0.f, 0.f};
+    float zra[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, zrb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float zrc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float u1 = 0.f, u2 = 0.f, u3 = 0.f;
+    auto obz = [&](int zz) {  // planes zs-6 .. ze+1 are asked for; only zs-2 .. ze+1 are used
+        zz = min(max(zz, -3), a.nz + 2);
+        return a.obst[((long long)zz * a.ny + y) * a.nx + x] != 0;
+    };
+    float in[Q3];
+    bool ob1 = obz(zs - 4), ob2 = obz(zs - 5), ob3 = obz(zs - 6);
+    {
+        const float *pl = a.fin + (long long)(zs - 3) * a.PL + row;
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) in[k] = pl[k * a.KS];
+    }
+    for (int j = zs - 3; j <= ze + 2; ++j) {
+        const float *pn = a.fin + (long long)min(j + 1, ze + 2) * a.PL + row;
+        ob3 = ob2;
+        ob2 = ob1;
+        ob1 = obz(j - 1);
+        float o1[Q3], o2[Q3], o3[Q3];
+        const float v1 = level3<T3TH3, TOL>(in, o1, lds1, j, r0a, r9aa, r9ba, zra, lane, wy, ob1, true, a);
+        if (own && j - 1 >= zs && j - 1 < ze) u1 += v1;
+        // level 1 is done with plane j: its registers take plane j + 1, in
+        // flight across levels 2 and 3
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) in[k] = pn[k * a.KS];
+        const float v2 = level3<T3TH3, TOL>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, zrb, lane, wy, ob2, true, a);
+        if (own && j - 2 >= zs && j - 2 < ze) u2 += v2;
+        const float v3 = level3<T3TH3, TOL>(o2, o3, lds3, j - 2, r0c, r9ac, r9bc, zrc, lane, wy, ob3, true, a);
+        if (own && j - 3 >= zs && j - 3 < ze) {
+            u3 += v3;
+            float *d = a.fout + (long long)(j - 3) * a.PL + row;
+#pragma unroll
+            for (int k = 0; k < Q3; ++k) __builtin_nontemporal_store(o3[k], d + k * a.KS);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        u1 += __shfl_down(u1, off, 64);
+        u2 += __shfl_down(u2, off, 64);
+        u3 += __shfl_down(u3, off, 64);
+    }
+    if (lane == 0) {
+        red[0][wy] = u1;
+        red[1][wy] = u2;
+        red[2][wy] = u3;
+    }
+    __syncthreads();
+    if (lane == 0 && wy == 0) {
+        float b1 = red[0][0], b2 = red[1][0], b3 = red[2][0];
+#pragma unroll
+        for (int i = 1; i < T3TH3; ++i) {
+            b1 += red[0][i];
+            b2 += red[1][i];
+            b3 += red[2][i];
+        }
+        const int blk = a.blk0 + (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        a.partials[blk] = b1;
+        a.partials[a.nblocks + blk] = b2;
+        a.partials[2 * a.nblocks + blk] = b3;
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void reduce3d(const float *partials, int n, float *av_local, int t) {
     __shared__ float lds[BLOCK / 64];
     const float v = sum_partials_n<BLOCK>(partials, n, lds);
@@ -681,11 +776,13 @@ struct Slab {
     bool f_joint = false;              // f[1] lies in f[0]'s allocation (LBM_LATTICE_PAD)
     float *o[2] = {nullptr, nullptr};  // origins: plane z = 0
     uint8_t *obst = nullptr;
-    uint8_t *obst_g = nullptr;   // [nzs + 4][ny][nx]: obst with two image planes each side (two-step kernel)
+    uint8_t *obst_g = nullptr;   // [nzs + 6][ny][nx]: obst with three image planes each side (two/three-step kernels)
     float *partials = nullptr;
     int nblk_all = 0, nblk_bnd = 0, nblk_int = 0;
     float *partials2 = nullptr;  // two-step kernel: [2][nblk_two]
     int nblk_two = 0;
+    float *partials3 = nullptr;  // three-step kernel (single slab): [3][nblk_three]
+    int nblk_three = 0;
     float *av_local = nullptr;
     int av_cap = 0;
     int cur = 0;
@@ -706,6 +803,13 @@ struct lbm3d_handle {
     int zb = 2;        // LBM3D_ZB: planes per block of the pair kernel (1, 2, 4, 8)
     bool nt = true;    // LBM3D_NT: non-temporal output stores
     bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two), single slab or z slabs
+    // LBM3D_THREE: three steps per pass (step3d_three), single slab (needs two);
+    // default (-1): in tolerance mode only -- 512^3: tolerance 50.2-50.6 vs
+    // 43.5-43.9 GLUPS for two-step passes, bitwise 43.9-44.1 vs 44.6-45.0 (the
+    // bitwise collision's divisions make the third level's recompute VALU-bound;
+    // profiles/r03/d3q19/ab_three.log)
+    int three = -1;
+    int seg3 = 64;     // LBM3D_SEG3: z planes per block of the three-step kernel
     int seg = 64;      // LBM3D_SEG: z planes per block of the two-step kernel (32-128 equal within noise at 512^3)
     int th = 12;       // LBM3D_TH: rows (waves) per block of the two-step kernel (12 only since round 3)
     bool skip = false; // LBM3D_SKIP: waves skip the collisions of rows no later level reads (not faster)
@@ -767,6 +871,8 @@ struct lbm3d_handle {
         if (const char *n = knob("LBM3D_NT")) nt = atoi(n) != 0;
         if (const char *t = knob("LBM3D_TWO")) two = atoi(t) != 0;
         if (const char *g = knob("LBM3D_SEG")) seg = std::max(1, atoi(g));
+        if (const char *t = knob("LBM3D_THREE")) three = atoi(t) != 0 ? 1 : 0;
+        if (const char *g = knob("LBM3D_SEG3")) seg3 = std::max(1, atoi(g));
         if (const char *h = knob("LBM3D_TH")) th = atoi(h);
         if (const char *k = knob("LBM3D_SKIP")) skip = atoi(k) != 0;
         if (const char *d = knob("LBM3D_PD")) pd = atoi(d);
@@ -860,7 +966,7 @@ struct lbm3d_handle {
         if (multi() || !use_two() || slabs.size() != 1) return;
         Slab &s = slabs[0];
         if ((long long)p.nx * p.ny * p.nz < probe_min_cells || s.f_joint) return;
-        const size_t floats = (size_t)(s.nzs + 4) * PL;
+        const size_t floats = (size_t)(s.nzs + 2 * GZ3) * PL;
         const size_t pair_bytes = 2 * sizeof(float) * floats;
         const int cap = (int)std::max<size_t>(1, (96ull << 30) / pair_bytes);
         const int tries = std::min({probe_tries, 8, cap});
@@ -871,7 +977,7 @@ struct lbm3d_handle {
         auto set_pair = [&](size_t c) {
             for (int k = 0; k < 2; ++k) {
                 s.f[k] = cand[c][k];
-                s.o[k] = s.f[k] + 2 * PL;
+                s.o[k] = s.f[k] + GZ3 * PL;
             }
             s.cur = 0;
         };
@@ -956,8 +1062,8 @@ struct lbm3d_handle {
         H3(hipDeviceGetStreamPriorityRange(&lo, &hi));
         H3(hipStreamCreateWithPriority(&s.s_bnd, hipStreamNonBlocking, hi));
         for (hipEvent_t *e : {&s.ev_b, &s.ev_i, &s.ev_x, &s.ev_end}) H3(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        // two ghost planes below and above (the two-step kernel reads both)
-        const size_t floats = (size_t)(s.nzs + 4) * PL;
+        // three ghost planes below and above (the three-step kernel reads all of them)
+        const size_t floats = (size_t)(s.nzs + 2 * GZ3) * PL;
         const char *lp = lattice_pad;
         if (lp && *lp) {
             // both lattices in one allocation, the second pad bytes (rounded to
@@ -974,14 +1080,14 @@ struct lbm3d_handle {
                 fill_fresh(s.f[k], floats * sizeof(float), s.s_comp);
             }
         }
-        for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + 2 * PL;
+        for (int k = 0; k < 2; ++k) s.o[k] = s.f[k] + GZ3 * PL;
         const size_t ob = (size_t)s.nzs * p.ny * p.nx, plane = (size_t)p.ny * p.nx;
         H3(hipMalloc(&s.obst, ob + 256));
         H3(hipMemcpy(s.obst, obstacles + (size_t)s.z0 * plane, ob, hipMemcpyHostToDevice));
-        H3(hipMalloc(&s.obst_g, (size_t)(s.nzs + 4) * plane + 256));
-        for (int z = -2; z < s.nzs + 2; ++z) {  // global periodic images (the neighbour slabs' planes)
+        H3(hipMalloc(&s.obst_g, (size_t)(s.nzs + 2 * GZ3) * plane + 256));
+        for (int z = -GZ3; z < s.nzs + GZ3; ++z) {  // global periodic images (the neighbour slabs' planes)
             const int gz = ((s.z0 + z) % p.nz + p.nz) % p.nz;
-            H3(hipMemcpy(s.obst_g + (size_t)(z + 2) * plane, obstacles + (size_t)gz * plane, plane,
+            H3(hipMemcpy(s.obst_g + (size_t)(z + GZ3) * plane, obstacles + (size_t)gz * plane, plane,
                          hipMemcpyHostToDevice));
         }
         // multi: two one-plane boundary launches, then the interior launch
@@ -994,6 +1100,11 @@ struct lbm3d_handle {
         for (const auto &r : two_ranges(s)) s.nblk_two += two_blocks(r.first, r.second);
         H3(hipMalloc(&s.partials2, sizeof(float) * (2 * (size_t)std::max(s.nblk_two, 1) + 64)));
         fill_fresh(s.partials2, sizeof(float) * (2 * (size_t)std::max(s.nblk_two, 1) + 64), s.s_comp);
+        s.nblk_three = multi() ? 0 : three_blocks(0, s.nzs);
+        if (s.nblk_three > 0) {
+            H3(hipMalloc(&s.partials3, sizeof(float) * (3 * (size_t)s.nblk_three + 64)));
+            fill_fresh(s.partials3, sizeof(float) * (3 * (size_t)s.nblk_three + 64), s.s_comp);
+        }
     }
 
     // Initial fill of a fresh allocation on `st`, waited for: zero, or with
@@ -1039,7 +1150,7 @@ struct lbm3d_handle {
         Two3Args a{};
         a.fin = s.o[s.cur];
         a.fout = s.o[1 - s.cur];
-        a.obst = s.obst_g + (size_t)2 * p.ny * p.nx;
+        a.obst = s.obst_g + (size_t)GZ3 * p.ny * p.nx;
         a.PL = PL;
         a.KS = KS;
         a.px = px;
@@ -1072,6 +1183,65 @@ struct lbm3d_handle {
             default: throw fail3(LBM_E_INTERNAL, "unvalidated two-step variant");
         }
         H3(hipGetLastError());
+    }
+
+    // three-step passes: one slab only (z slabs keep the two-plane exchange)
+    bool use_three() const { return (three < 0 ? tolerance : three != 0) && use_two() && !multi(); }
+    int three_blocks(int z0, int zn) const {
+        return ((p.nx + T3OX3 - 1) / T3OX3) * ((p.ny + T3OY3 - 1) / T3OY3) * ((zn - z0 + seg3 - 1) / seg3);
+    }
+
+    void launch_three(Slab &s, hipStream_t st) {
+        Two3Args a{};
+        a.fin = s.o[s.cur];
+        a.fout = s.o[1 - s.cur];
+        a.obst = s.obst_g + (size_t)GZ3 * p.ny * p.nx;
+        a.PL = PL;
+        a.KS = KS;
+        a.px = px;
+        a.nx = p.nx;
+        a.ny = p.ny;
+        a.nz = s.nzs;
+        a.seg = seg3;
+        a.z0 = 0;
+        a.zn = s.nzs;
+        a.omega = p.omega;
+        a.omo = 1 - p.omega;
+        a.w1 = w1();
+        a.w2 = w2();
+        a.k0 = p.omega * (1.f / 3.f);
+        a.k1 = p.omega * (1.f / 18.f);
+        a.k2 = p.omega * (1.f / 36.f);
+        a.partials = s.partials3;
+        a.nblocks = s.nblk_three;
+        a.blk0 = 0;
+        const dim3 g((p.nx + T3OX3 - 1) / T3OX3, (p.ny + T3OY3 - 1) / T3OY3, (s.nzs + seg3 - 1) / seg3);
+        const dim3 b(T3W, T3TH3);
+        if (tolerance)
+            hipLaunchKernelGGL((step3d_three<true>), g, b, 0, st, a);
+        else
+            hipLaunchKernelGGL((step3d_three<false>), g, b, 0, st, a);
+        H3(hipGetLastError());
+    }
+
+    // three-step pass (single slab): ghost planes -3..-1, nz..nz+2 of the
+    // current lattice (periodic images, all 19 speeds), step3d_three, then the
+    // three steps' |u|
+    void step_three(int t) {
+        Slab &s = slabs[0];
+        const size_t bytes = sizeof(float) * (size_t)PL;
+        float *o = s.o[s.cur];
+        for (int g : {-3, -2, -1, s.nzs, s.nzs + 1, s.nzs + 2}) {
+            const int src = ((g % s.nzs) + s.nzs) % s.nzs;
+            H3(hipMemcpyAsync(o + (long long)g * PL, o + (long long)src * PL, bytes, hipMemcpyDeviceToDevice, s.s_comp));
+        }
+        launch_three(s, s.s_comp);
+        for (int l = 0; l < 3; ++l)
+            hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials3 + (size_t)l * s.nblk_three,
+                               s.nblk_three, s.av_local, t + l);
+        H3(hipGetLastError());
+        s.cur ^= 1;
+        exchange(s.cur, false);  // faces for a one-step launch that may follow
     }
 
     void reduce_two(Slab &s, int t, hipStream_t st) {
@@ -1366,6 +1536,8 @@ struct lbm3d_handle {
                 }
                 exchange2(slabs[0].cur, false);
             }
+            if (use_three())
+                for (; t + 3 <= steps; t += 3) step_three(t);
             for (; t + 2 <= steps; t += 2) step_two(t);
         }
         for (; t < steps; ++t) step_once(t);
@@ -1390,7 +1562,7 @@ struct lbm3d_handle {
         for (auto &s : slabs) {
             H3(hipSetDevice(s.dev));
             s.cur = 0;
-            const long long planes = s.nzs + 4;
+            const long long planes = s.nzs + 2 * GZ3;
             hipLaunchKernelGGL(init3d, dim3((unsigned)((planes * KS + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s.s_comp,
                                s.f[0], planes, KS, PL, c0, c1, c2);
             H3(hipGetLastError());
@@ -1480,6 +1652,7 @@ struct lbm3d_handle {
             if (s.obst_g) (void)hipFree(s.obst_g);
             if (s.partials) (void)hipFree(s.partials);
             if (s.partials2) (void)hipFree(s.partials2);
+            if (s.partials3) (void)hipFree(s.partials3);
             if (s.av_local) (void)hipFree(s.av_local);
             for (hipStream_t st : {s.s_comp, s.s_bnd, s.s_comm})
                 if (st) (void)hipStreamDestroy(st);

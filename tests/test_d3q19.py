@@ -102,7 +102,9 @@ def _gpu3d(native, p, obst, c0, steps, **kw):
 def test_d3q19_bitwise_single_slab(gpu_lib, nx, ny, nz, pair, two, seg, monkeypatch):
     """Column-pair kernel (even nx) and one-cell kernel, and the two-steps-per-pass
     kernel (z segments of 32, 2 and 1 planes; 9 steps = four two-step passes + one
-    one-step launch), partial blocks in x, y, z, wrapped tiles (nx < 60)."""
+    one-step launch), partial blocks in x, y, z, wrapped tiles (nx < 60).  The
+    three-step pass is off here (test_d3q19_three_step_bitwise covers it)."""
+    monkeypatch.setenv("LBM3D_THREE", "0")
     monkeypatch.setenv("LBM3D_PAIR", pair)
     monkeypatch.setenv("LBM3D_TWO", two)
     monkeypatch.setenv("LBM3D_SEG", seg)
@@ -185,24 +187,28 @@ def test_d3q19_256cube_steps_and_mass(gpu_lib):
 @pytest.mark.gpu
 def test_d3q19_512cube_64bit_indexing(gpu_lib, monkeypatch):
     """BASELINE config 5's 512^3 on one GPU: 2.55e9 floats per lattice (over 2^31),
-    so every index into it must be 64-bit.  3 steps as one two-step pass plus one
-    pair-kernel step, and as three one-cell steps (independent indexing code):
-    bitwise equal, finite."""
+    so every index into it must be 64-bit.  3 steps as one three-step pass, as
+    one two-step pass plus one pair-kernel step, and as three one-cell steps
+    (independent indexing code): bitwise equal, finite."""
     n = 512
     p = lio.Params3D(n, n, n, 0, 0.1, 0.001, 1.85)
     obst = lio.channel_obstacles3d(n, n, n)
     out = {}
-    for pair, two in (("1", "1"), ("0", "0")):  # two-step passes + pair kernel; one-cell kernel
+    monkeypatch.setenv("LBM3D_PLACEMENT_TRIES", "1")
+    for pair, two, three in (("1", "1", "1"), ("1", "1", "0"), ("0", "0", "0")):
         monkeypatch.setenv("LBM3D_PAIR", pair)
         monkeypatch.setenv("LBM3D_TWO", two)
+        monkeypatch.setenv("LBM3D_THREE", three)
         with gpu_lib.Engine3D(p, obst, devices=[0]) as e:
             e.init_equilibrium()
             e.run_steps(3)
-            out[pair] = e.store(n_av=3)
-    (a, av_a), (b, av_b) = out["1"], out["0"]
+            out[pair + two + three] = e.store(n_av=3)
+    a, av_a = out["111"]
     assert np.isfinite(a[::31, ::29, ::37]).all()
-    assert np.array_equal(a, b)
-    np.testing.assert_allclose(av_a, av_b, rtol=1e-5)
+    for key in ("110", "000"):
+        b, av_b = out[key]
+        assert np.array_equal(a, b), key
+        np.testing.assert_allclose(av_a, av_b, rtol=1e-5)
 
 
 @pytest.mark.gpu
@@ -246,6 +252,7 @@ def test_d3q19_two_step_block_rows_bitwise(gpu_lib, nx, ny, nz, parts, th, skip,
     prefetched a whole iteration ahead): bitwise vs the oracle on partial and
     wrapped tiles (ny below and above one block's owned rows), one slab and
     z slabs, 9 steps (four passes + one one-step launch)."""
+    monkeypatch.setenv("LBM3D_THREE", "0")
     monkeypatch.setenv("LBM3D_TH", th)
     monkeypatch.setenv("LBM3D_SKIP", skip)
     monkeypatch.setenv("LBM3D_PD", pd)
@@ -255,6 +262,53 @@ def test_d3q19_two_step_block_rows_bitwise(gpu_lib, nx, ny, nz, parts, th, skip,
     cells, av = _gpu3d(gpu_lib, p, obst, c0, 9, parts=parts, devices=[0])
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg3", ["64", "5", "1"])
+@pytest.mark.parametrize("nx,ny,nz", [(13, 9, 7), (64, 8, 5), (1, 5, 3), (130, 3, 2), (61, 17, 1), (125, 23, 9),
+                                      (58, 6, 4), (59, 13, 12), (2, 6, 3)])
+def test_d3q19_three_step_bitwise(gpu_lib, nx, ny, nz, seg3, monkeypatch):
+    """Three steps per pass (step3d_three, single slab, the default there):
+    10 steps = three passes + one one-step launch, 8 = two passes + one
+    two-step pass; owned tiles of 58 x 6 (partial and wrapped in x and y:
+    nx, ny below and above one tile), z segments of 64, 5 and 1 planes, slabs
+    thinner than the three ghost planes (nz < 3).  Bitwise vs the oracle
+    (LBM3D_THREE=1: by default the three-step pass runs in tolerance mode only)."""
+    monkeypatch.setenv("LBM3D_THREE", "1")
+    monkeypatch.setenv("LBM3D_SEG3", seg3)
+    p, obst, c0 = _problem(nx, ny, nz, 3 * nx + ny + nz)
+    for steps in (10, 8):
+        ref, ref_av = oracle.run3d(p, obst, steps, c0)
+        cells, av = _gpu3d(gpu_lib, p, obst, c0, steps, devices=[0])
+        assert np.array_equal(cells, ref), steps
+        np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_d3q19_three_step_reruns_and_tolerance(gpu_lib, monkeypatch):
+    """The three-step pass across runs (state carried over, ghost planes
+    refreshed per pass: 4 + 5 + 6 steps bitwise equal to the oracle's 15),
+    and in tolerance mode (6 steps) within 2e-5 relative of the oracle and
+    bitwise equal to the two-step passes' tolerance lattice (same per-cell
+    arithmetic, other pass structure)."""
+    monkeypatch.setenv("LBM3D_THREE", "1")
+    p, obst, c0 = _problem(70, 31, 24, 7)
+    ref, _ = oracle.run3d(p, obst, 15, c0)
+    with gpu_lib.Engine3D(p, obst, devices=[0]) as e:
+        e.load_cells(c0)
+        for n in (4, 5, 6):
+            e.run_steps(n)
+        cells, _ = e.store()
+    assert np.array_equal(cells, ref)
+    # 6 steps: two three-step passes / three two-step passes (a one-step
+    # launch would use the bitwise pair kernel in both modes)
+    ref6, _ = oracle.run3d(p, obst, 6, c0)
+    tol3, _ = _gpu3d(gpu_lib, p, obst, c0, 6, devices=[0], flags=gpu_lib.FLAG_TOLERANCE)
+    dev = float(np.max(np.abs(tol3.astype(np.float64) - ref6) / np.maximum(np.abs(ref6), 1e-30)))
+    assert dev < 2e-5, dev
+    tol2, _ = _gpu3d(gpu_lib, p, obst, c0, 6, parts=3, devices=[0], flags=gpu_lib.FLAG_TOLERANCE)
+    assert np.array_equal(tol3, tol2)
 
 
 @pytest.mark.gpu

@@ -1,7 +1,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
-K="LBM_DEBUG_KNOBS=1"
-V=""
-for s in 2 3 4 5 6 7 8; do V="$V --variant t$s:FLAGS=4,$K,LBM_TOL_S=$s"; done
-for s in 2 3 4 5 6; do V="$V --variant b$s:$K,LBM_STREAM_S=$s"; done
-bash tools/gpu_steps.sh "500|ab_spl_ow16|python3 tools/ab_bench.py --n 8192 --steps 840 --warmup 24 --rounds 2 $V"
-grep variant gpurun_out/ab_spl_ow16.log | cut -c1-20,110-230
+export LBM_DEBUG_KNOBS=1
+B="python3 tools/bench3d.py --n 512 --steps 60 --rounds 3"
+bash tools/gpu_steps.sh \
+  "500|ab_three|LBM3D_THREE=0 $B && LBM3D_THREE=1 $B && LBM3D_THREE=1 LBM3D_SEG3=128 $B && LBM3D_THREE=0 $B --flags 4 && LBM3D_THREE=1 $B --flags 4 && LBM3D_THREE=1 LBM3D_SEG3=128 $B --flags 4 && LBM3D_THREE=0 $B && LBM3D_THREE=1 $B && LBM3D_THREE=0 $B --flags 4 && LBM3D_THREE=1 $B --flags 4"
+cat gpurun_out/ab_three.log | grep mlups
