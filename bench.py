@@ -339,17 +339,24 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
     cells = n ** 3
     # two steps per pass (step3d_two: 60 x 8 owned of 64 x 12 loaded cells per
     # plane -> (19 x 4 B x (768/480 + 1)) / 2 = 98.8 B per update) on one slab and
-    # on z slabs of >= 4 planes; 152 B per update for the one-step kernel
+    # on z slabs of >= 4 planes; 152 B per update for the one-step kernel; one
+    # slab in tolerance mode: three steps per pass (step3d_three: 58 x 6 owned
+    # -> (19 x 4 B x (768/348 + 1)) / 3 = 81.2 B), the rest in two-step passes
     two = nzs >= 4
-    alg_b = 19 * 4 * (768 / 480 + 1) / 2 if two else 152
+    three = two and not dist_on and bool(flags & native.FLAG_TOLERANCE)
+    b2, b3 = 19 * 4 * (768 / 480 + 1) / 2, 19 * 4 * (768 / 348 + 1) / 3
+    n3 = steps // 3 * 3 if three else 0
+    n2 = (steps - n3) // 2 * 2 if two else 0
+    alg_b = (n3 * b3 + n2 * b2 + (steps - n3 - n2) * 152) / max(steps, 1)
     per_gpu_gbs = alg_b * cells / world * steps / dev / 1e9
     return {"grid": f"{n}^3", "steps": steps, "settle_steps": nset, "decomposition": f"{world} z slabs",
             "numerics": "tolerance" if flags & native.FLAG_TOLERANCE else "bitwise",
-            "kernel": "step3d_two (2 steps per pass)" if two else "step3d_pair (1 step per launch)",
+            "kernel": (f"step3d_three ({n3 // 3} passes of 3 steps) + step3d_two ({n2 // 2} of 2)" if three else
+                       "step3d_two (2 steps per pass)" if two else "step3d_pair (1 step per launch)"),
             "mlups": round(cells * steps / secs / 1e6, 1), "ms_per_step": round(secs / steps * 1e3, 4),
             "hbm_gbs_per_gpu": round(per_gpu_gbs, 1), "hbm_frac": round(per_gpu_gbs / HBM_PEAK_GBS, 4),
             "effective_gbs_per_gpu": round(152 * cells / world * steps / dev / 1e9, 1),
-            "note": f"{alg_b:.1f} algorithmic B per update (152 = 19 fp32 loads + stores per step; effective_gbs on "
+            "note": f"{alg_b:.1f} algorithmic B per update, mean over the passes (152 = 19 fp32 loads + stores per step; effective_gbs on "
                     "that basis); parity unpinned upstream (no 3-D reference)"}
 
 
