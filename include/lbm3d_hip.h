@@ -31,15 +31,17 @@
  *   opposite: 1<->2, 3<->4, 5<->6, 7<->8, 9+i <-> 14+i (i = 0..4).
  *
  * Layout at the boundary: AoS float[nz][ny][nx][19]; obstacles uint8[nz][ny][nx].
- * Inside: per z plane all 19 populations, f[z+1][k][y][px], with one ghost
- * plane below and above; the domain is cut into z slabs (one per rank /
- * sub-domain), and after every step each slab's top plane speeds 9..13 and
- * bottom plane speeds 14..18 move to the neighbour's ghost planes.
+ * Inside: per z plane all 19 populations, f[z+3][k][y][px], with three ghost
+ * planes below and above; the domain is cut into z slabs (one per rank /
+ * sub-domain); one-step launches move each slab's top plane speeds 9..13 and
+ * bottom plane speeds 14..18 to the neighbour's ghost planes, two-step passes
+ * two whole planes each way, and a single slab in tolerance mode runs three
+ * steps per pass (its ghost planes refreshed from the periodic images).
  *
  * Placement reuses lbm_config (lbm_hip.h): parts = z slabs, transport LOCAL
  * (all slabs in this process, device copies) or RCCL (one slab per rank);
  * kernel / graph fields are ignored; flags may carry LBM_FLAG_TOLERANCE: the
- * two-step passes then use the reciprocal collision (one v_rcp_f32 + Newton
+ * two- and three-step passes then use the reciprocal collision (one v_rcp_f32 + Newton
  * step for u, FMA contraction; not bitwise equal to the restatement, within
  * the tolerance tests/test_d3q19.py states), one-step launches stay bitwise.
  */
