@@ -21,5 +21,8 @@ bash tools/gpu_steps.sh \
   "300|prof_trace|rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o drv --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-aux" \
   "120|pmc_fetch|timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1 --variant tol:FLAGS=4" \
   "120|pmc_write|timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1 --variant tol:FLAGS=4" \
-  "120|pmc_sq|timeout -s KILL 100 rocprofv3 --pmc $SQ -d gpurun_out/pmc_sq -o sq --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1 --variant tol:FLAGS=4"
+  "120|pmc_sq|timeout -s KILL 100 rocprofv3 --pmc $SQ -d gpurun_out/pmc_sq -o sq --output-format csv -- python3 tools/ab_bench.py --n 8192 --steps 42 --warmup 6 --rounds 1 --variant tol:FLAGS=4" \
+  "200|d3_trace|rocprofv3 --kernel-trace --stats -d gpurun_out/d3_trace -o d3 --output-format csv -- python3 tools/bench3d.py --n 512 --steps 30 --flags 4" \
+  "150|d3_fetch|timeout -s KILL 140 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/d3_fetch -o fetch --output-format csv -- python3 tools/bench3d.py --n 512 --steps 12 --warmup 0 --flags 4" \
+  "150|d3_write|timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/d3_write -o write --output-format csv -- python3 tools/bench3d.py --n 512 --steps 12 --warmup 0 --flags 4"
 grep -h "passed\|failed" gpurun_out/pytest_gpu.log; tail -n 2 gpurun_out/smoke.log; tail -n 1 gpurun_out/bench.log
