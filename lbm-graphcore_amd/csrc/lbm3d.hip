@@ -803,7 +803,8 @@ struct lbm3d_handle {
     int zb = 2;        // LBM3D_ZB: planes per block of the pair kernel (1, 2, 4, 8)
     bool nt = true;    // LBM3D_NT: non-temporal output stores
     bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two), single slab or z slabs
-    // LBM3D_THREE: three steps per pass (step3d_three), single slab (needs two);
+    // LBM3D_THREE: three steps per pass (step3d_three), one slab or z slabs of
+    // >= 6 planes (needs two);
     // default (-1): in tolerance mode only -- 512^3: tolerance 50.2-50.6 vs
     // 43.5-43.9 GLUPS for two-step passes, bitwise 43.9-44.1 vs 44.6-45.0 (the
     // bitwise collision's divisions make the third level's recompute VALU-bound;
@@ -1100,7 +1101,8 @@ struct lbm3d_handle {
         for (const auto &r : two_ranges(s)) s.nblk_two += two_blocks(r.first, r.second);
         H3(hipMalloc(&s.partials2, sizeof(float) * (2 * (size_t)std::max(s.nblk_two, 1) + 64)));
         fill_fresh(s.partials2, sizeof(float) * (2 * (size_t)std::max(s.nblk_two, 1) + 64), s.s_comp);
-        s.nblk_three = multi() ? 0 : three_blocks(0, s.nzs);
+        s.nblk_three = 0;
+        for (const auto &r : three_ranges(s)) s.nblk_three += three_blocks(r.first, r.second);
         if (s.nblk_three > 0) {
             H3(hipMalloc(&s.partials3, sizeof(float) * (3 * (size_t)s.nblk_three + 64)));
             fill_fresh(s.partials3, sizeof(float) * (3 * (size_t)s.nblk_three + 64), s.s_comp);
@@ -1185,13 +1187,28 @@ struct lbm3d_handle {
         H3(hipGetLastError());
     }
 
-    // three-step passes: one slab only (z slabs keep the two-plane exchange)
-    bool use_three() const { return (three < 0 ? tolerance : three != 0) && use_two() && !multi(); }
+    // three-step passes: one slab, or z slabs of at least 6 planes (ghosts are
+    // 3 planes of the neighbours, exchanged once per pass)
+    bool use_three() const {
+        if (!(three < 0 ? tolerance : three != 0) || !use_two()) return false;
+        if (!multi()) return true;
+        for (int n : all_nz)
+            if (n < 6) return false;
+        return true;
+    }
     int three_blocks(int z0, int zn) const {
         return ((p.nx + T3OX3 - 1) / T3OX3) * ((p.ny + T3OY3 - 1) / T3OY3) * ((zn - z0 + seg3 - 1) / seg3);
     }
+    // output plane ranges of one three-step pass, in launch order (as two_ranges)
+    std::vector<std::pair<int, int>> three_ranges(const Slab &s) const {
+        if (!multi() || s.nzs < 6) return {{0, s.nzs}};
+        std::vector<std::pair<int, int>> r = {{0, 3}, {s.nzs - 3, s.nzs}};
+        if (s.nzs > 6) r.push_back({3, s.nzs - 3});
+        return r;
+    }
 
-    void launch_three(Slab &s, hipStream_t st) {
+    void launch_three(Slab &s, int z0, int zn, int blk0, hipStream_t st) {
+        if (zn <= z0) return;
         Two3Args a{};
         a.fin = s.o[s.cur];
         a.fout = s.o[1 - s.cur];
@@ -1203,8 +1220,8 @@ struct lbm3d_handle {
         a.ny = p.ny;
         a.nz = s.nzs;
         a.seg = seg3;
-        a.z0 = 0;
-        a.zn = s.nzs;
+        a.z0 = z0;
+        a.zn = zn;
         a.omega = p.omega;
         a.omo = 1 - p.omega;
         a.w1 = w1();
@@ -1214,8 +1231,8 @@ struct lbm3d_handle {
         a.k2 = p.omega * (1.f / 36.f);
         a.partials = s.partials3;
         a.nblocks = s.nblk_three;
-        a.blk0 = 0;
-        const dim3 g((p.nx + T3OX3 - 1) / T3OX3, (p.ny + T3OY3 - 1) / T3OY3, (s.nzs + seg3 - 1) / seg3);
+        a.blk0 = blk0;
+        const dim3 g((p.nx + T3OX3 - 1) / T3OX3, (p.ny + T3OY3 - 1) / T3OY3, (zn - z0 + seg3 - 1) / seg3);
         const dim3 b(T3W, T3TH3);
         if (tolerance)
             hipLaunchKernelGGL((step3d_three<true>), g, b, 0, st, a);
@@ -1227,7 +1244,47 @@ struct lbm3d_handle {
     // three-step pass (single slab): ghost planes -3..-1, nz..nz+2 of the
     // current lattice (periodic images, all 19 speeds), step3d_three, then the
     // three steps' |u|
+    void reduce_three(Slab &s, int t, hipStream_t st) {
+        for (int l = 0; l < 3; ++l)
+            hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, st, s.partials3 + (size_t)l * s.nblk_three,
+                               s.nblk_three, s.av_local, t + l);
+        H3(hipGetLastError());
+    }
+
+    // Three steps of every slab (z slabs): as step_two_multi with three-plane
+    // boundary ranges and a three-plane exchange.
+    void step_three_multi(int t) {
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            H3(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
+            wait_x(s, s.s_bnd);
+            const auto r = three_ranges(s);
+            int blk = 0;
+            for (size_t i = 0; i < r.size() && i < 2; ++i) {
+                launch_three(s, r[i].first, r[i].second, blk, s.s_bnd);
+                blk += three_blocks(r[i].first, r[i].second);
+            }
+            H3(hipEventRecord(s.ev_b, s.s_bnd));
+        }
+        exchange_planes(1 - slabs[0].cur, 3, true);
+        for (auto &s : slabs) {
+            H3(hipSetDevice(s.dev));
+            const auto r = three_ranges(s);
+            if (r.size() > 2)
+                launch_three(s, r[2].first, r[2].second,
+                             three_blocks(r[0].first, r[0].second) + three_blocks(r[1].first, r[1].second), s.s_comp);
+            H3(hipStreamWaitEvent(s.s_comp, s.ev_b, 0));
+            reduce_three(s, t, s.s_comp);
+            H3(hipEventRecord(s.ev_i, s.s_comp));
+            s.cur ^= 1;
+        }
+    }
+
     void step_three(int t) {
+        if (multi()) {
+            step_three_multi(t);
+            return;
+        }
         Slab &s = slabs[0];
         const size_t bytes = sizeof(float) * (size_t)PL;
         float *o = s.o[s.cur];
@@ -1235,11 +1292,8 @@ struct lbm3d_handle {
             const int src = ((g % s.nzs) + s.nzs) % s.nzs;
             H3(hipMemcpyAsync(o + (long long)g * PL, o + (long long)src * PL, bytes, hipMemcpyDeviceToDevice, s.s_comp));
         }
-        launch_three(s, s.s_comp);
-        for (int l = 0; l < 3; ++l)
-            hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials3 + (size_t)l * s.nblk_three,
-                               s.nblk_three, s.av_local, t + l);
-        H3(hipGetLastError());
+        launch_three(s, 0, s.nzs, 0, s.s_comp);
+        reduce_three(s, t, s.s_comp);
         s.cur ^= 1;
         exchange(s.cur, false);  // faces for a one-step launch that may follow
     }
@@ -1251,15 +1305,17 @@ struct lbm3d_handle {
         H3(hipGetLastError());
     }
 
-    // Two-plane ghost exchange of lattice l (all 19 speeds): planes nzs-2,
-    // nzs-1 go up into the next slab's ghosts -2, -1; planes 0, 1 go down into
-    // the previous slab's ghosts nzs, nzs+1.  Every rank posts send up, send
-    // down, recv from below, recv from above (RCCL matches by order).
-    void exchange2(int l, bool use_comm) {
-        const size_t n2 = 2 * (size_t)PL;
-        auto top = [&](const Slab &s) { return s.o[l] + (long long)(s.nzs - 2) * PL; };
+    // n-plane ghost exchange of lattice l (all 19 speeds; n = 2 for two-step,
+    // 3 for three-step passes): planes nzs-n .. nzs-1 go up into the next
+    // slab's ghosts -n .. -1; planes 0 .. n-1 go down into the previous slab's
+    // ghosts nzs .. nzs+n-1.  Every rank posts send up, send down, recv from
+    // below, recv from above (RCCL matches by order).
+    void exchange2(int l, bool use_comm) { exchange_planes(l, 2, use_comm); }
+    void exchange_planes(int l, int n, bool use_comm) {
+        const size_t n2 = (size_t)n * PL;
+        auto top = [&](const Slab &s) { return s.o[l] + (long long)(s.nzs - n) * PL; };
         auto bottom = [&](const Slab &s) { return s.o[l]; };
-        auto ghost_lo = [&](const Slab &s) { return s.o[l] - 2 * PL; };
+        auto ghost_lo = [&](const Slab &s) { return s.o[l] - n * PL; };
         auto ghost_hi = [&](const Slab &s) { return s.o[l] + (long long)s.nzs * PL; };
         if (transport == LBM_TRANSPORT_RCCL) {
             Slab &s = slabs[0];
@@ -1529,12 +1585,12 @@ struct lbm3d_handle {
         }
         int t = 0;
         if (use_two() && steps >= 2) {
-            if (multi()) {  // two-plane ghosts of the current lattice (a one-step launch leaves only its five speeds)
+            if (multi()) {  // two- / three-plane ghosts of the current lattice (a one-step launch leaves only its five speeds)
                 for (auto &s : slabs) {
                     H3(hipSetDevice(s.dev));
                     H3(hipEventRecord(s.ev_b, s.s_comp));
                 }
-                exchange2(slabs[0].cur, false);
+                exchange_planes(slabs[0].cur, use_three() && steps >= 3 ? 3 : 2, false);
             }
             if (use_three())
                 for (; t + 3 <= steps; t += 3) step_three(t);

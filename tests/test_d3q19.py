@@ -307,8 +307,41 @@ def test_d3q19_three_step_reruns_and_tolerance(gpu_lib, monkeypatch):
     tol3, _ = _gpu3d(gpu_lib, p, obst, c0, 6, devices=[0], flags=gpu_lib.FLAG_TOLERANCE)
     dev = float(np.max(np.abs(tol3.astype(np.float64) - ref6) / np.maximum(np.abs(ref6), 1e-30)))
     assert dev < 2e-5, dev
+    monkeypatch.setenv("LBM3D_THREE", "0")
     tol2, _ = _gpu3d(gpu_lib, p, obst, c0, 6, parts=3, devices=[0], flags=gpu_lib.FLAG_TOLERANCE)
     assert np.array_equal(tol3, tol2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,seg3", [(2, "64"), (3, "5"), (4, "1"), (6, "64"), (7, "64")])
+def test_d3q19_slabs_three_step_bitwise(gpu_lib, parts, seg3, monkeypatch):
+    """Three steps per pass on z slabs: the boundary plane triples first, a
+    three-plane exchange (all 19 speeds) overlapped with the interior; 10
+    steps = three passes + one one-step launch, 8 = two passes + a two-step
+    pass.  Ragged slabs of 5..20 planes (7 slabs: some below 6 planes, so the
+    engine keeps two-step passes), z segments of 1..64 planes."""
+    monkeypatch.setenv("LBM3D_THREE", "1")
+    monkeypatch.setenv("LBM3D_SEG3", seg3)
+    p, obst, c0 = _problem(22, 9, 40, 200 + parts)
+    for steps in (10, 8):
+        ref, ref_av = oracle.run3d(p, obst, steps, c0)
+        cells, av = _gpu3d(gpu_lib, p, obst, c0, steps, parts=parts, devices=[0])
+        assert np.array_equal(cells, ref), steps
+        np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_d3q19_rccl_three_step_self_exchange_bitwise(gpu_lib, monkeypatch):
+    """World of one over RCCL with three-step passes: the three-plane ghost
+    triples go through ncclSend / ncclRecv to itself once per pass."""
+    monkeypatch.setenv("LBM3D_THREE", "1")
+    p, obst, c0 = _problem(24, 10, 12, 19)
+    for steps in (6, 7, 8):
+        ref, ref_av = oracle.run3d(p, obst, steps, c0)
+        cells, av = _gpu3d(gpu_lib, p, obst, c0, steps, transport=gpu_lib.TRANSPORT_RCCL, rank=0, world=1,
+                           devices=[0], unique_id=gpu_lib.rccl_unique_id())
+        assert np.array_equal(cells, ref), steps
+        np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
 @pytest.mark.gpu
@@ -336,8 +369,9 @@ def test_d3q19_lattice_placement_bitwise(gpu_lib, nx, ny, nz, parts, two, env, m
 def test_d3q19_tolerance_vs_oracle(gpu_lib, parts):
     """LBM_FLAG_TOLERANCE (cell3dt in the two-step passes): every population
     within 2e-5 relative of the restatement after 8 steps (four two-step
-    passes), av_vels within 1e-4, and the tolerance result does not depend on
-    the slab decomposition (bitwise equal to one slab)."""
+    passes; three-step passes where the slabs allow them), av_vels within 1e-4,
+    and the tolerance result does not depend on the slab decomposition (bitwise
+    equal to one slab)."""
     p, obst, c0 = _problem(70, 31, 24, 99)
     ref, ref_av = oracle.run3d(p, obst, 8, c0)
     one, _ = _gpu3d(gpu_lib, p, obst, c0, 8, devices=[0], flags=gpu_lib.FLAG_TOLERANCE)
