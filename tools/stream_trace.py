@@ -56,13 +56,14 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--slots", type=int, default=2048, help="resident waves the device holds (2/SIMD x 1024)")
+    ap.add_argument("--flags", type=int, default=0, help="lbm_config flags (4 = LBM_FLAG_TOLERANCE: S = 7)")
     a = ap.parse_args()
     p = lio.Params(a.n, a.n, a.steps, 10, 0.1, 0.005, 1.85)
     obst = synthetic_obstacles(a.n, a.n)
     with tempfile.TemporaryDirectory() as wd:
         path = os.path.join(wd, "trace.bin")
         os.environ["LBM_STREAM_TRACE"] = path
-        with native.Engine(p, obst, devices=[0]) as e:
+        with native.Engine(p, obst, devices=[0], flags=a.flags) as e:
             e.init_equilibrium()
             e.run_steps(16, accelerate_first=True)
             e.run_steps(a.steps)
@@ -70,6 +71,7 @@ def main():
         tr = np.fromfile(path, dtype=np.uint64).reshape(-1, 2)
     out = analyse(tr, a.slots)
     out["ms_per_launch_events"] = round(ms, 4)
+    out["flags"] = a.flags
     out["env"] = {k: v for k, v in os.environ.items() if k.startswith("LBM_") and k != "LBM_STREAM_TRACE"}
     print(json.dumps(out), flush=True)
 
