@@ -96,3 +96,32 @@ def test_d3q19_512_eight_slabs_bitwise(gpu_lib):
     np.testing.assert_allclose(eight[1], one[1], rtol=1e-4)
     np.testing.assert_allclose(eight[3], one[3], rtol=1e-4)
     assert np.isfinite(eight[2][::37, ::31, ::29]).all()
+
+
+@pytest.mark.gpu
+def test_d3q19_512_eight_slabs_tolerance_three_step(gpu_lib):
+    """BASELINE config 5's shape in tolerance mode: three-step passes on one
+    slab (periodic ghost refresh) and on 8 z slabs of 64 planes (three-plane
+    exchange per pass, boundary triples first) -- 7 steps = two three-step
+    passes + a one-step launch, then 6 more (two passes): bitwise equal lattices,
+    finite, mass conserved."""
+    n = 512
+    p = lio.Params3D(n, n, n, 4, 0.1, 0.001, 1.85)
+    obst = lio.channel_obstacles3d(n, n, n)
+    outs = {}
+    for parts in (1, 8):
+        with gpu_lib.Engine3D(p, obst, parts=parts, devices=[0], flags=gpu_lib.FLAG_TOLERANCE) as e:
+            e.init_equilibrium()
+            e.run_steps(7)
+            c7, av7 = e.store(n_av=7)
+            e.run_steps(6)
+            c13, av13 = e.store(n_av=6)
+        outs[parts] = (c7, av7, c13, av13)
+    one, eight = outs[1], outs[8]
+    assert np.array_equal(eight[0], one[0])
+    assert np.array_equal(eight[2], one[2])
+    np.testing.assert_allclose(eight[1], one[1], rtol=1e-4)
+    np.testing.assert_allclose(eight[3], one[3], rtol=1e-4)
+    assert np.isfinite(eight[2][::37, ::31, ::29]).all()
+    m0 = float(one[0].sum(dtype=np.float64))
+    assert float(one[2].sum(dtype=np.float64)) == pytest.approx(m0, rel=1e-5)
