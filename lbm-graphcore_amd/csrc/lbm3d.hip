@@ -957,8 +957,8 @@ struct lbm3d_handle {
     // +-5 % at 512^3 fixed by where the lattices land (39.9-44.2 GLUPS over
     // six engines in one process, profiles/r03/d3q19/spread.log).  A single
     // slab of at least 2^26 cells allocates up to probe_tries lattice pairs
-    // (at most 96 GB held at once: four at 512^3), times the passes the runs
-    // will use (three-step in tolerance mode) on each (constant populations; one warm-up round, then the best of two
+    // (at most 96 GB held at once: four at 512^3), times two-step passes on
+    // each (constant populations; one warm-up round, then the best of two
     // interleaved rounds), keeps the fastest pair and frees the rest; the kept
     // pair is filled as a fresh allocation is, so the engine's state is as if
     // the probe had not run.  Failures inside free every extra candidate and
@@ -1003,11 +1003,8 @@ struct lbm3d_handle {
                 for (size_t c = 0; c < cand.size(); ++c) {
                     set_pair(c);
                     H3(hipEventRecord(e0, s.s_comp));
-                    for (int i = 0; i < 2; ++i) {  // the pass the runs will use
-                        if (use_three())
-                            launch_three(s, 0, s.nzs, 0, s.s_comp);
-                        else
-                            launch_two(s, 0, s.nzs, 0, s.s_comp);
+                    for (int i = 0; i < 2; ++i) {
+                        launch_two(s, 0, s.nzs, 0, s.s_comp);
                         s.cur ^= 1;
                     }
                     H3(hipEventRecord(e1, s.s_comp));
@@ -1019,8 +1016,7 @@ struct lbm3d_handle {
             for (size_t c = 1; c < cand.size(); ++c)
                 if (best[c] < best[keep]) keep = c;
             if (probe_log) {
-                fprintf(stderr, "lbm3d placement probe (%dx%dx%d): ms per %s-step pass", p.nx, p.ny, p.nz,
-                        use_three() ? "three" : "two");
+                fprintf(stderr, "lbm3d placement probe (%dx%dx%d): ms per two-step pass", p.nx, p.ny, p.nz);
                 for (float v : best) fprintf(stderr, " %.4f", v);
                 fprintf(stderr, "; kept pair %zu\n", keep);
             }
