@@ -278,6 +278,8 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
         kernel_used = e.kernel_in_use()
         spl = e.steps_per_launch()
         rect = e.local_rects()[0]
+        _, av = e.store(cells=False, n_av=steps)
+    finite = _agree_max(0 if np.isfinite(av).all() else 1, dist_on) == 0
     if dist_on:
         import torch
         t = torch.tensor([secs], dtype=torch.float64)
@@ -287,8 +289,10 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
     return {"grid": f"{n}x{n}", "steps": steps, "settle_steps": nset,
             "decomposition": f"{R}x{C}" + (" (y slabs)" if slabs else " (reference partitionForIpus rule)"),
             "sub_domain": f"{rect[2]}x{rect[3]}", "kernel": kernel_used, "numerics": numerics,
-            "launches": launch_plan(steps, spl, kernel_used == "stream"),
-            "mlups": round(n * n * steps / secs / 1e6, 1), "ms_per_step": round(secs / steps * 1e3, 4)}
+            "launches": launch_plan(steps, spl, kernel_used == "stream"), "av_vels_finite": finite,
+            # no rate for a run whose av_vels went non-finite (a broken lattice is not a measurement)
+            "mlups": round(n * n * steps / secs / 1e6, 1) if finite else None,
+            "ms_per_step": round(secs / steps * 1e3, 4)}
 
 
 def _agree_max(v: int, dist_on: bool) -> int:
@@ -331,6 +335,8 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
         secs = time.perf_counter() - t0
         dev = e.last_run_seconds()
         nzs = e.local_slabs()[0][1]
+        _, av = e.store(cells=False, n_av=steps)
+    finite = _agree_max(0 if np.isfinite(av).all() else 1, dist_on) == 0
     if dist_on:
         import torch
         t = torch.tensor([secs, dev], dtype=torch.float64)
@@ -353,60 +359,128 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
             "numerics": "tolerance" if flags & native.FLAG_TOLERANCE else "bitwise",
             "kernel": (f"step3d_three ({n3 // 3} passes of 3 steps) + step3d_two ({n2 // 2} of 2)" if three else
                        "step3d_two (2 steps per pass)" if two else "step3d_pair (1 step per launch)"),
-            "mlups": round(cells * steps / secs / 1e6, 1), "ms_per_step": round(secs / steps * 1e3, 4),
+            "av_vels_finite": finite, "mlups": round(cells * steps / secs / 1e6, 1) if finite else None,
+            "ms_per_step": round(secs / steps * 1e3, 4),
             "hbm_gbs_per_gpu": round(per_gpu_gbs, 1), "hbm_frac": round(per_gpu_gbs / HBM_PEAK_GBS, 4),
             "effective_gbs_per_gpu": round(152 * cells / world * steps / dev / 1e9, 1),
             "note": f"{alg_b:.1f} algorithmic B per update, mean over the passes (152 = 19 fp32 loads + stores per step; effective_gbs on "
                     "that basis); parity unpinned upstream (no 3-D reference)"}
 
 
-def multi_rank_check(rank: int, world: int, local_rank: int, n: int = 2048) -> dict:
+def _check_cases(world: int):
+    """The multi-rank self-check's cases: (name, global nx, ny, grid (R, C) or (0, 0) for the
+    reference rule, numerics, steps, flags, perturbed start)."""
+    n = 2048
+    # config 4's per-rank shape at a quarter of its height: 16384^2 over N ranks
+    # by the reference rule is (16384 / C) x (16384 / R) per rank (4096 x 8192 in
+    # 2x4 at N = 8); the check runs (16384 / C) x (4096 / R) per rank (4096 x 2048)
+    # on the same R x C grid, with the tolerance collision's driver plan
+    # (7 + 7 + a fused 6-step remainder)
+    R4, C4, _ = native.partition(16384, 16384, world)
+    cases = []
+    for mode, steps, flags in (("bitwise", 13, 0), ("tolerance", 20, native.FLAG_TOLERANCE)):
+        for name, grid in (("reference_rule", (0, 0)), ("slabs", (world, 1))):
+            cases.append((f"{mode}_{name}", n, n, grid, mode, steps, flags, True))
+    cases.append(("tolerance_config4_shape", 16384, 4096, (R4, C4), "tolerance", 20, native.FLAG_TOLERANCE, False))
+    return cases
+
+
+def multi_rank_check(rank: int, world: int, local_rank: int) -> dict:
     """N > 1, untimed, before the timed region: the fused stream kernel over all
-    ranks (RCCL halos, the reference partitionForIpus blocks and N x 1 slabs)
-    on an n^2 problem with random obstacles and a perturbed initial state --
-    bitwise collision, 13 steps (two 6-step launches + a one-step remainder),
-    and tolerance collision, 20 steps (7 + 7 + a fused 6-step remainder, the
-    driver's timed plan) -- gathered on rank 0 and compared bitwise with a
-    single-domain run of the same library and mode on rank 0's GPU
-    (tests/test_gpu_parity.py pins the bitwise one to the CPU oracle; the
-    tolerance collision is decomposition-invariant, tests/test_gpu_tolerance.py).
+    ranks (RCCL halos) against a single-domain run of the same library and mode
+    on every rank's own GPU (each rank compares its own block bitwise; no
+    gather).  Cases (_check_cases): a 2048^2 problem with random obstacles and a
+    perturbed start on the reference partitionForIpus blocks and on N x 1 slabs,
+    bitwise collision 13 steps (two 6-step launches + a one-step remainder) and
+    tolerance collision 20 steps (7 + 7 + a fused 6-step remainder, the driver's
+    timed plan); and config 4's per-rank block shape (a quarter of its height:
+    4096 x 2048 per rank in 2x4 at N = 8) in tolerance mode, 20 steps.
+    tests/test_gpu_parity.py pins the bitwise collision to the CPU oracle; the
+    tolerance collision is decomposition-invariant (tests/test_gpu_tolerance.py).
+    Every rank runs the same collective sequence whatever happens on it: an
+    exception in a case is recorded as that rank's result and the per-case
+    all_gather_object still runs.  (A rank that fails inside an RCCL call
+    leaves the others waiting; bench's main watchdog ends that, exit 4.)
     Reference: StructuredGridUtils.hpp:498-522 (split), :805-851 (halos)."""
     import torch.distributed as dist
-    rng = np.random.default_rng(2024)
-    obst = synthetic_obstacles(n, n)
-    obst[rng.random((n, n)) < 0.02] = 1
-    p0 = lio.Params(n, n, 1, 10, 0.1, 0.005, 1.85)
-    cells0 = (lio.init_cells(p0) * (1 + 0.02 * rng.standard_normal((n, n, 9)))).astype(np.float32)
     results = {}
-    for mode, steps, flags in (("bitwise", 13, 0), ("tolerance", 20, native.FLAG_TOLERANCE)):
-        p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
-        for name, grid in (("reference_rule", (0, 0)), ("slabs", (world, 1))):
-            box = [native.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(box, src=0)
+    for name, nx, ny, grid, mode, steps, flags, perturbed in _check_cases(world):
+        rng = np.random.default_rng(2024)
+        obst = synthetic_obstacles(nx, ny)
+        obst[rng.random((ny, nx)) < 0.02] = 1
+        p = lio.Params(nx, ny, steps, 10, 0.1, 0.005, 1.85)
+        cells0 = (lio.init_cells(p) * (1 + 0.02 * rng.standard_normal((ny, nx, 9)))).astype(np.float32) \
+            if perturbed else None
+        box = [native.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        mine = {"bitwise": False}
+        try:
+            R, C, rects = native.partition(nx, ny, world, *grid)
+            x0, y0, w, h = (int(v) for v in rects[rank])
             with native.Engine(p, obst, parts=world, grid=grid, transport=native.TRANSPORT_RCCL, rank=rank,
                                world=world, devices=[local_rank], unique_id=box[0], kernel=native.KERNEL_STREAM,
                                flags=flags) as e:
-                rects = lio_rects = [tuple(r) for r in native.partition(n, n, world, *grid)[2]]
-                x0, y0, w, h = rects[rank]
-                e.load_cells_local([cells0[y0:y0 + h, x0:x0 + w]])
+                if perturbed:
+                    e.load_cells_local([cells0[y0:y0 + h, x0:x0 + w]])
+                else:
+                    e.init_equilibrium()
                 e.run_steps(steps, accelerate_first=True)
                 stats = e.run_stats()
                 blocks, av = e.store_local(n_av=steps)
-            full = lio.gather_subdomains(blocks[0], lio_rects, n, n)
-            if rank == 0:
-                with native.Engine(p, obst, devices=[local_rank], kernel=native.KERNEL_STREAM, flags=flags) as e1:
+            with native.Engine(p, obst, devices=[local_rank], kernel=native.KERNEL_STREAM, flags=flags) as e1:
+                if perturbed:
                     e1.load_cells(cells0)
-                    e1.run_steps(steps, accelerate_first=True)
-                    ref, ref_av = e1.store(n_av=steps)
-                results[f"{mode}_{name}"] = {
-                    "decomposition": "x".join(map(str, native.partition(n, n, world, *grid)[:2])), "steps": steps,
-                    "bitwise": bool(np.array_equal(full, ref)), "launches": list(stats),
+                else:
+                    e1.init_equilibrium()
+                e1.run_steps(steps, accelerate_first=True)
+                ref, ref_av = e1.store(n_av=steps)
+            mine = {"decomposition": f"{R}x{C}", "block": f"{w}x{h}", "steps": steps, "launches": list(stats),
+                    "bitwise": bool(np.array_equal(blocks[0], ref[y0:y0 + h, x0:x0 + w])),
+                    "finite": bool(np.isfinite(blocks[0]).all() and np.isfinite(av).all()),
                     "av_vels_rel": float(np.max(np.abs(av - ref_av) / np.abs(ref_av)))}
-    ok = [False]
+            mine["bitwise"] = mine["bitwise"] and mine["finite"]
+        except Exception as exc:  # recorded; the collective sequence continues
+            mine = {"bitwise": False, "error": f"{type(exc).__name__}: {exc}"}
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        bad = [r for r, m in enumerate(every) if not m.get("bitwise")]
+        results[name] = dict(every[0], ranks_failed=bad)
+        if bad:
+            results[name]["bitwise"] = False
+            errors = {r: every[r]["error"] for r in bad if every[r].get("error")}
+            if errors:
+                results[name]["errors"] = errors
+    return {"passed": all(not r["ranks_failed"] for r in results.values()), "cases": results}
+
+
+CHECK_FAILED_EXIT = 5
+
+
+def gate_multi_rank(mrc: dict, rank: int, n: int, mwd=None) -> None:
+    """A failed self-check is fatal before anything is timed: rank 0 prints
+    check_failed_line (value null, the cases) and every rank exits with
+    CHECK_FAILED_EXIT (5).  Every rank already holds the same per-case verdict
+    (all_gather_object); an exception outside the cases is local to one rank,
+    so the ranks agree on the outcome explicitly first."""
+    ok = _agree_max(0 if mrc.get("passed") else 1, True) == 0
+    if ok:
+        return
     if rank == 0:
-        ok = [all(r["bitwise"] for r in results.values())]
-    dist.broadcast_object_list(ok, src=0)
-    return {"passed": bool(ok[0]), "grid": f"{n}x{n}", "cases": results}
+        print(json.dumps(check_failed_line(mrc, n)), flush=True)
+    log(f"multi-rank self-check failed; exiting with status {CHECK_FAILED_EXIT} before the timed region")
+    if mwd is not None:
+        mwd.cancel()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(CHECK_FAILED_EXIT)
+
+
+def check_failed_line(mrc: dict, n: int) -> dict:
+    """The line printed (rank 0) when the multi-rank self-check fails: no value."""
+    return {"metric": METRIC, "value": None, "unit": "MLUPS", "n_gpus": n, "higher_is_better": True,
+            "error": "multi-rank self-check failed: the decomposed run differs from the single-domain run "
+                     "(or raised); nothing was timed",
+            "multi_rank_bitwise": False, "multi_rank_check": mrc}
 
 
 # Device ms per fused launch of S steps at 8192^2 (profiles/r03/ab_spl_ow16.log,
@@ -642,8 +716,9 @@ def main() -> int:
         try:
             mrc = multi_rank_check(rank, world, local_rank)
         except Exception as exc:  # recorded, never silently dropped
-            mrc = {"passed": False, "error": str(exc)}
+            mrc = {"passed": False, "error": f"{type(exc).__name__}: {exc}"}
         log(f"multi-rank bitwise check: {mrc}")
+        gate_multi_rank(mrc, rank, n, mwd)
     tol_main = args.numerics == "tolerance" and args.kernel in ("auto", "stream")
     kflags_main = kflags | (native.FLAG_TOLERANCE if tol_main else 0)
     m = measure_weak(tnx, tny, R, C, args, kernel, kflags_main, rank, world, local_rank, dist_on)

@@ -68,7 +68,12 @@ typedef struct lbm3d_params {
 
 typedef struct lbm3d_handle lbm3d_handle;
 
-/* Create the engine: obstacles uint8[nz][ny][nx] (full domain). */
+/* Create the engine: obstacles uint8[nz][ny][nx] (full domain).
+ * Bitwise-mode single-slab engines of >= 2^26 cells run a placement probe
+ * here: up to four candidate lattice pairs, at most
+ * 96 GB of device memory held transiently (about 82 GB at 512^3), the fastest
+ * kept and the rest freed before the call returns.  Tolerance-mode engines
+ * (three-step passes) skip it. */
 int lbm3d_create(const lbm3d_params *params, const uint8_t *obstacles, const lbm_config *config,
                  lbm3d_handle **out);
 

@@ -963,8 +963,12 @@ struct lbm3d_handle {
     // pair is filled as a fresh allocation is, so the engine's state is as if
     // the probe had not run.  Failures inside free every extra candidate and
     // restore the original pair.
+    // Scope: bitwise-mode engines (two-step passes).  Tolerance-mode runs use
+    // three-step passes, whose spread over lattice placements has not been
+    // measured to follow the two-step pass's, so they skip the probe (and its
+    // transient ~82 GB of candidate pairs at 512^3).
     void placement_probe() {
-        if (multi() || !use_two() || slabs.size() != 1) return;
+        if (multi() || !use_two() || use_three() || slabs.size() != 1) return;
         Slab &s = slabs[0];
         if ((long long)p.nx * p.ny * p.nz < probe_min_cells || s.f_joint) return;
         const size_t floats = (size_t)(s.nzs + 2 * GZ3) * PL;

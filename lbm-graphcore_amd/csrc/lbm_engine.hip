@@ -312,7 +312,7 @@ struct lbm_handle {
         graph_steps = std::max(0, knob("LBM_GRAPH_STEPS", graph_steps));
         fused = knob("LBM_TWO_STEP", fused ? 1 : 0) != 0;
         tile2 = std::min(std::max(knob("LBM_TILE2", tile2), -1), NUM_TILE2 - 1);
-        xoff = std::max(MAX_GR, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
+        xoff = std::max(MIN_XOFF, (knob("LBM_XOFF", xoff) + 3) / 4 * 4);
         stream_s = std::min(std::max(knob("LBM_STREAM_S", stream_s), 2), 6);
         stream_hs = std::max(0, knob("LBM_STREAM_HS", stream_hs));
         auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
@@ -1415,6 +1415,12 @@ struct lbm_handle {
                             p = nullptr;
                         }
         };
+        hipEvent_t e0 = nullptr, e1 = nullptr;  // outside the try: the catch destroys them too
+        auto drop_events = [&]() {
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+            e0 = e1 = nullptr;
+        };
         try {
             for (int c = 1; c < tries; ++c) {
                 std::array<float *, 2> f{nullptr, nullptr};
@@ -1430,7 +1436,6 @@ struct lbm_handle {
             for (auto &f : cand)
                 for (float *p : f)
                     HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), (int)fill, n, s.s_comp));
-            hipEvent_t e0 = nullptr, e1 = nullptr;
             HIP_CHECK(hipEventCreate(&e0));
             HIP_CHECK(hipEventCreate(&e1));
             std::vector<float> best(cand.size(), 1e30f);
@@ -1451,8 +1456,7 @@ struct lbm_handle {
                     HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
                     best[c] = std::min(best[c], ms / timed);
                 }
-            HIP_CHECK(hipEventDestroy(e0));
-            HIP_CHECK(hipEventDestroy(e1));
+            drop_events();
             for (size_t c = 1; c < cand.size(); ++c)
                 if (best[c] < best[keep]) keep = c;
             // LBM_PLACEMENT_KEEP=k (tests): keep candidate k whatever the timings,
@@ -1477,6 +1481,7 @@ struct lbm_handle {
             for (float *p : cand[keep]) fill_fresh(p, sizeof(float) * n, s.s_comp);
             build_args(s);
         } catch (...) {
+            drop_events();
             // keep == 0 here unless the failure came after the choice; either way
             // the handle ends up owning exactly one pair
             unwind();
@@ -1662,12 +1667,6 @@ struct lbm_handle {
             run_single = steps;
             return;
         }
-        // a ring left partial by the previous run's remainder launch is rebuilt
-        // first (outside this run's device timer: it is the previous run's work)
-        if (ring_stale) {
-            refresh_halos();
-            ring_stale = false;
-        }
         for (auto &s : subs) {  // stream-ordered before this run's first launch
             set_device(s);
             HIP_CHECK(hipMemsetAsync(s.ctl, 0, 64, s.s_comp));
@@ -1686,6 +1685,13 @@ struct lbm_handle {
                 set_device(subs[k]);
                 HIP_CHECK(hipStreamWaitEvent(subs[k].s_comp, t0, 0));
             }
+        // a ring left partial by the previous run's remainder launch is rebuilt
+        // first, inside this run's device timer: every run that needs the
+        // rebuild pays for it exactly once (lbm_last_run_seconds)
+        if (ring_stale) {
+            refresh_halos();
+            ring_stale = false;
+        }
         if (accelerate_first && p.ny >= 2) {
             const float w1 = p.density * p.accel / 9.f;
             const float w2 = p.density * p.accel / 36.f;

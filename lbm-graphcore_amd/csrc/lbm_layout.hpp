@@ -34,7 +34,10 @@ namespace lbm {
 
 constexpr int Q = 9;
 constexpr int XOFF = 4;   // interior column 0 offset inside a plane row
-constexpr int MAX_GR = 6;  // widest ghost ring (rows/columns) any kernel needs (stream kernel, S <= 6)
+constexpr int MAX_GR = 8;  // widest ghost ring (rows/columns) any kernel needs (stream kernel: S <= 8, tolerance)
+// smallest interior column offset: an odd-S strip reads S + 1 columns left of
+// column 0 (float2 alignment), and rows must stay 16-B aligned
+constexpr int MIN_XOFF = (MAX_GR + 2 + 3) / 4 * 4;
 constexpr int BLOCK = 256;  // 4 wave64s
 constexpr int MAX_RECTS = 4;
 constexpr int MAX_SRECTS = 32;  // stream kernels: guided per-XCD row bands (lbm_engine.hip stream_split)

@@ -34,24 +34,27 @@ def _obstacles_2d(n):
     return o
 
 
-def _run_2d(native, p, obst, **kw):
-    """8 steps (accelerated first), store; 6 more, store.  Returns both lattices + av_vels."""
+def _run_2d(native, p, obst, steps=(8, 6), **kw):
+    """steps[0] steps (accelerated first), store; steps[1] more, store.  Returns
+    both lattices + av_vels and the launch counts of both runs."""
     with native.Engine(p, obst, devices=[0], **kw) as e:
         e.init_equilibrium()
-        e.run_steps(8, accelerate_first=True)
-        a8, av8 = e.store(n_av=8)
-        e.run_steps(6)
-        a14, av14 = e.store(n_av=6)
+        e.run_steps(steps[0], accelerate_first=True)
+        stats = [e.run_stats()]
+        a8, av8 = e.store(n_av=steps[0])
+        e.run_steps(steps[1])
+        stats.append(e.run_stats())
+        a14, av14 = e.store(n_av=steps[1])
         kernel = e.kernel_in_use()
         rects = e.local_rects()
-    return kernel, rects, (a8, av8), (a14, av14)
+    return kernel, rects, (a8, av8), (a14, av14), stats
 
 
 @pytest.fixture(scope="module")
 def single_16384(gpu_lib):
     p = lio.Params(N2, N2, 8, 10, 0.1, 0.005, 1.85)
     obst = _obstacles_2d(N2)
-    kernel, rects, s8, s14 = _run_2d(gpu_lib, p, obst)
+    kernel, rects, s8, s14, _ = _run_2d(gpu_lib, p, obst)
     assert kernel == "stream" and len(rects) == 1
     assert np.isfinite(s14[0][::251, ::241]).all()
     return p, obst, s8, s14
@@ -66,7 +69,7 @@ def test_16384_eight_subdomains_bitwise(gpu_lib, single_16384, grid):
         kw = dict(parts=8)
     else:
         kw = dict(parts=8, grid=grid)
-    kernel, rects, d8, d14 = _run_2d(gpu_lib, p, obst, **kw)
+    kernel, rects, d8, d14, _ = _run_2d(gpu_lib, p, obst, **kw)
     assert kernel == "stream" and len(rects) == 8
     assert {(r[2], r[3]) for r in rects} == {(N2 // grid[1], N2 // grid[0])}
     assert np.array_equal(d8[0], s8[0]), "after 8 steps (two fused launches)"
@@ -74,6 +77,38 @@ def test_16384_eight_subdomains_bitwise(gpu_lib, single_16384, grid):
     assert np.array_equal(d14[0], s14[0]), "after 6 more (fused launch + one-step remainder)"
     np.testing.assert_allclose(d14[1], s14[1], rtol=1e-4)
     assert np.isfinite(d14[0][::251, ::241]).all()
+
+
+TOL_STEPS = (9, 13)  # S = 7: 7 + a fused 2-step remainder, then 7 + a fused 6-step remainder
+
+
+@pytest.fixture(scope="module")
+def single_16384_tolerance(gpu_lib):
+    p = lio.Params(N2, N2, 9, 10, 0.1, 0.005, 1.85)
+    obst = _obstacles_2d(N2)
+    kernel, rects, s9, s22, stats = _run_2d(gpu_lib, p, obst, steps=TOL_STEPS, flags=gpu_lib.FLAG_TOLERANCE)
+    assert kernel == "stream" and len(rects) == 1
+    assert stats == [(2, 0), (2, 0)]
+    assert np.isfinite(s22[0][::251, ::241]).all()
+    return p, obst, s9, s22
+
+
+@pytest.mark.parametrize("grid", [(2, 4), (8, 1)], ids=["2x4-reference-rule", "8x1-slabs"])
+def test_16384_eight_subdomains_tolerance_bitwise(gpu_lib, single_16384_tolerance, grid):
+    """The tolerance plan bench.py publishes for config 4 (S = 7 launches and
+    fused remainders), decomposed as the 8-GPU runs decompose it, against its
+    single-domain run: the tolerance collision is the same per-cell arithmetic
+    everywhere, so the lattices must be bitwise equal."""
+    p, obst, s9, s22 = single_16384_tolerance
+    kw = dict(parts=8) if grid == (2, 4) else dict(parts=8, grid=grid)
+    kernel, rects, d9, d22, stats = _run_2d(gpu_lib, p, obst, steps=TOL_STEPS, flags=gpu_lib.FLAG_TOLERANCE, **kw)
+    assert kernel == "stream" and len(rects) == 8
+    assert {(r[2], r[3]) for r in rects} == {(N2 // grid[1], N2 // grid[0])}
+    assert stats == [(2, 0), (2, 0)]
+    assert np.array_equal(d9[0], s9[0]), "after 9 steps (7 + fused 2)"
+    np.testing.assert_allclose(d9[1], s9[1], rtol=1e-4)
+    assert np.array_equal(d22[0], s22[0]), "after 13 more (7 + fused 6)"
+    np.testing.assert_allclose(d22[1], s22[1], rtol=1e-4)
 
 
 def test_d3q19_512_eight_slabs_bitwise(gpu_lib):

@@ -31,8 +31,15 @@ def _tol_kw(gpu_lib, **kw):
     return dict(kernel=gpu_lib.KERNEL_STREAM, flags=gpu_lib.FLAG_TOLERANCE, **kw)
 
 
-def _rel(a, b):
-    return float(np.max(np.abs(a.astype(np.float64) - b) / np.maximum(np.abs(b.astype(np.float64)), 1e-30)))
+def _rel(a, b, chunk=1 << 26):
+    """max |a - b| / |b| over every element (float64, in chunks: a 16384^2
+    lattice holds 2.4e9 floats)."""
+    a, b = a.reshape(-1), b.reshape(-1)
+    worst = 0.0
+    for i in range(0, a.size, chunk):
+        x, y = a[i:i + chunk].astype(np.float64), b[i:i + chunk].astype(np.float64)
+        worst = max(worst, float(np.max(np.abs(x - y) / np.maximum(np.abs(y), 1e-30))))
+    return worst
 
 
 @pytest.mark.parametrize("kernel", ["stream", "resident"])
@@ -85,6 +92,36 @@ def test_tolerance_8192_vs_oracle(gpu_lib):
     print(f"8192^2, 100 steps: populations max relative deviation {dev:.3e}, av_vels {dav:.3e}")
     assert dev < TOL_POP
     assert dav < 2e-3  # includes the oracle's own sequential-sum drift over 67M terms (bitwise mode: 2e-3 too)
+
+
+def test_tolerance_16384_vs_oracle(gpu_lib):
+    """BASELINE config 4's grid in the mode bench.py publishes for it
+    (aux.config4_16384x16384): single domain, tolerance collision, default
+    S = 7, placement probe on.  9 steps = one 7-step launch + ONE fused 2-step
+    remainder launch; one lattice holds 2.4e9 floats (over 2^31), so every
+    index of the LP form and of the remainder launch must be 64-bit.  Every
+    population within TOL_POP of the oracle."""
+    n = 16384
+    p = lio.Params(n, n, 9, 10, 0.1, 0.005, 1.85)
+    obst = np.zeros((n, n), np.uint8)
+    obst[0, :] = obst[-1, :] = 1
+    obst[:, 0] = obst[:, -1] = 1
+    obst[:, n // 3] = 1
+    with gpu_lib.Engine(p, obst, flags=gpu_lib.FLAG_TOLERANCE) as e:
+        assert e.kernel_in_use() == "stream" and e.numerics() == "tolerance"
+        assert e.steps_per_launch() == 7
+        e.init_equilibrium()
+        e.run_steps(9, accelerate_first=True)
+        assert e.run_stats() == (2, 0)
+        cells, av = e.store(n_av=9)
+    assert np.isfinite(av).all()
+    ref, ref_av = oracle.run_mt(p, obst, 9, 16, lio.init_cells(p))
+    dev = _rel(cells, ref)
+    del cells, ref
+    dav = float(np.max(np.abs(av - ref_av) / np.abs(ref_av)))
+    print(f"16384^2, 9 steps (7 + fused 2): populations max relative deviation {dev:.3e}, av_vels {dav:.3e}")
+    assert dev < TOL_POP
+    assert dav < 5e-3  # 268M-term sequential fp32 sums in the oracle (bitwise mode: 5e-3 too)
 
 
 def test_tolerance_decomposition_invariant(gpu_lib):
