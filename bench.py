@@ -47,7 +47,7 @@ over ranks.  value = all cells x K / seconds / 1e6 (whole job).
 
 roofline: 72 algorithmic bytes per cell per LAUNCH (9 fp32 loads + 9 fp32
 stores; the 1-byte obstacle mask is excluded) -- a fused launch advances
-steps_per_launch time steps (S = 7 for the tolerance value at K = 20 or 1000)
+steps_per_launch time steps (S = 10 for the tolerance value at K = 20 or 1000)
 but moves the lattice through HBM once -- divided by the average launch duration measured
 with HIP events recorded by the library on the kernel's own stream over the
 timed region (device time of the K steps / launches); peak = 8000 GB/s
@@ -374,11 +374,10 @@ def _check_cases(world: int):
     # config 4's per-rank shape at a quarter of its height: 16384^2 over N ranks
     # by the reference rule is (16384 / C) x (16384 / R) per rank (4096 x 8192 in
     # 2x4 at N = 8); the check runs (16384 / C) x (4096 / R) per rank (4096 x 2048)
-    # on the same R x C grid, with the tolerance collision's driver plan
-    # (7 + 7 + a fused 6-step remainder)
+    # on the same R x C grid, with the tolerance collision's driver plan (2 x 10)
     R4, C4, _ = native.partition(16384, 16384, world)
     cases = []
-    for mode, steps, flags in (("bitwise", 13, 0), ("tolerance", 20, native.FLAG_TOLERANCE)):
+    for mode, steps, flags in (("bitwise", 13, 0), ("tolerance", 27, native.FLAG_TOLERANCE)):
         for name, grid in (("reference_rule", (0, 0)), ("slabs", (world, 1))):
             cases.append((f"{mode}_{name}", n, n, grid, mode, steps, flags, True))
     cases.append(("tolerance_config4_shape", 16384, 4096, (R4, C4), "tolerance", 20, native.FLAG_TOLERANCE, False))
@@ -392,9 +391,10 @@ def multi_rank_check(rank: int, world: int, local_rank: int) -> dict:
     gather).  Cases (_check_cases): a 2048^2 problem with random obstacles and a
     perturbed start on the reference partitionForIpus blocks and on N x 1 slabs,
     bitwise collision 13 steps (two 6-step launches + a one-step remainder) and
-    tolerance collision 20 steps (7 + 7 + a fused 6-step remainder, the driver's
-    timed plan); and config 4's per-rank block shape (a quarter of its height:
-    4096 x 2048 per rank in 2x4 at N = 8) in tolerance mode, 20 steps.
+    tolerance collision 27 steps (10 + 10 + a fused 7-step remainder); and
+    config 4's per-rank block shape (a quarter of its height: 4096 x 2048 per
+    rank in 2x4 at N = 8) in tolerance mode, 20 steps (2 x 10, the driver's
+    timed plan).
     tests/test_gpu_parity.py pins the bitwise collision to the CPU oracle; the
     tolerance collision is decomposition-invariant (tests/test_gpu_tolerance.py).
     Every rank runs the same collective sequence whatever happens on it: an
@@ -484,11 +484,12 @@ def check_failed_line(mrc: dict, n: int) -> dict:
 
 
 # Device ms per fused launch of S steps at 8192^2 (profiles/r03/ab_spl_ow16.log,
-# 16-column aligned strips): bitwise and tolerance collision; a launch of
-# 2..5 steps is bound by the lattice pass (~1.1 ms); a one-step (vec4)
-# launch 0.81 ms.
+# 16-column aligned strips; tolerance S >= 7: the round-4 LP form with one row
+# per iteration, profiles/r04/ab_lp10.log): bitwise and tolerance collision; a
+# launch of 2..5 steps is bound by the lattice pass (~1.1 ms); a one-step
+# (vec4) launch 0.81 ms.
 LAUNCH_MS = {"bitwise": {2: 1.12, 3: 1.07, 4: 1.10, 5: 1.18, 6: 1.39},
-             "tolerance": {2: 1.11, 3: 1.07, 4: 1.08, 5: 1.10, 6: 1.10, 7: 1.13, 8: 1.52}}
+             "tolerance": {2: 1.11, 3: 1.07, 4: 1.08, 5: 1.10, 6: 1.10, 7: 1.21, 8: 1.33, 9: 1.50, 10: 1.55}}
 ONE_STEP_MS = 0.81
 
 
@@ -498,7 +499,7 @@ def pick_spl(steps: int, requested: int, numerics: str = "bitwise", fused_remain
     the remainder steps % S as the library runs it (include/lbm_hip.h: one
     fused launch when >= 2 steps, else one one-step launch) -- bitwise: the
     driver's 20-step run is four 5-step launches, 1000 steps 166 six-step
-    launches + a 4-step one; tolerance: 7 + 7 + 6 and 142 x 7 + 6."""
+    launches + a 4-step one; tolerance: 2 x 10 and 100 x 10."""
     if requested:
         return requested
     ms = LAUNCH_MS[numerics]
@@ -671,7 +672,7 @@ def main() -> int:
                     help="stream: fused S-step register-streaming kernel; step2: fused two-step LDS kernel; "
                          "vec4/scalar: one step per launch; auto: the library's choice")
     ap.add_argument("--spl", type=int, default=0,
-                    help="stream: time steps per launch (2..6, 2..8 with tolerance numerics; 0 = the fastest for "
+                    help="stream: time steps per launch (2..6, 2..10 with tolerance numerics; 0 = the fastest for "
                          "--steps by the measured launch times, pick_spl)")
     ap.add_argument("--numerics", default="tolerance", choices=["tolerance", "bitwise"],
                     help="value's collision: tolerance = LBM_FLAG_TOLERANCE (fp32, within the stated tolerance of "

@@ -56,8 +56,8 @@ typedef struct lbm_params {
 enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
 /* Step kernels.  SCALAR / VEC4: one time step per launch (VEC4 needs widths
  * that are multiples of 4).  STEP2: fused two-step launches through LDS.
- * STREAM: fused S-step launches (S = steps_per_launch, 2..6, 2..8 with
- * LBM_FLAG_TOLERANCE; default 6, 7 with it) streaming rows through registers; a run of
+ * STREAM: fused S-step launches (S = steps_per_launch, 2..6, 2..10 with
+ * LBM_FLAG_TOLERANCE; default 6, 10 with it) streaming rows through registers; a run of
  * K steps is K / S launches plus, when 2 <= K % S, one fused launch of K % S
  * steps (else K % S one-step launches), single and decomposed domains alike.  RESIDENT: every step of a run in one persistent
  * launch with the lattice held on chip (LDS + registers) -- single
@@ -108,8 +108,8 @@ typedef struct lbm_config {
     int32_t graph_steps;    /* >0: replay the step loop as hipGraphs of 2*graph_steps steps
                                (single sub-domain without exchange); <0: off; 0: library default */
     int32_t flags;          /* LBM_FLAG_* */
-    int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..6; 2..8 with LBM_FLAG_TOLERANCE);
-                                 0 = library default (6; 7 with LBM_FLAG_TOLERANCE) */
+    int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..6; 2..10 with LBM_FLAG_TOLERANCE);
+                                 0 = library default (6; 10 with LBM_FLAG_TOLERANCE) */
 } lbm_config;
 
 /* Route the periodic wrap of undecomposed dimensions through the transport

@@ -199,11 +199,11 @@ struct lbm_handle {
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     bool guide_set = false;                    // guide given by LBM_STREAM_GUIDE (else by S at create)
     int stream_cfg = 4;      // LBM_STREAM_CFG (launch form, one wave per workgroup): 0 plain stores;
-                             // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 8)
+                             // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 10)
     // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
-    // (S = 7, LP form: 386 vs 336 GLUPS at S = 6 and 365 at S = 8, which spills;
-    // profiles/r03/deep_tol/ab96.log)
-    int tol_s = 7, tol_cfg = 4;
+    // (S = 10, LP form, one row per iteration: 0.155 vs 0.183 ms per step for
+    // S = 7 and 0.174 for S = 8 at 8192^2; profiles/r04/ab_lp10.log)
+    int tol_s = 10, tol_cfg = 4;
     int env_kernel = -1;     // LBM_KERNEL: overrides an AUTO kernel request
     long long stream_min_cells = 4LL << 20;  // LBM_STREAM_MIN_CELLS: AUTO picks the stream kernel for sub-domains
                                              // at least this large (smaller ones lack waves for it: step2)
@@ -318,7 +318,7 @@ struct lbm_handle {
         auto form = [](int c, int dflt) { return (c == 0 || c == 3 || c == 4) ? c : dflt; };
         stream_cfg = form(knob("LBM_STREAM_CFG", stream_cfg), stream_cfg);
         tol_cfg = form(knob("LBM_TOL_CFG", tol_cfg), tol_cfg);
-        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 8);
+        tol_s = std::min(std::max(knob("LBM_TOL_S", tol_s), 2), 10);
         stream_min_cells = std::max(0, knob("LBM_STREAM_MIN_CELLS", (int)stream_min_cells));
         if (const char *g = knob_str("LBM_STREAM_GUIDE")) set_guide(g);
         res_th_env = std::max(0, knob("LBM_RES_TH", 0));
@@ -690,7 +690,10 @@ struct lbm_handle {
         // extra recomputed columns (8192^2: tolerance S = 4 / 6 +6 / +8 %,
         // bitwise S = 5 +6 %; bitwise S = 6, VALU-bound, -4 % and keeps the
         // natural width; profiles/r03/ab_ow16.log)
-        const bool ow16 = knob("LBM_STREAM_OW16", (tolerance || S <= 5) ? 1 : 0) != 0;
+        // S = 9, 10 (tolerance): 128 - 2S rounds down to 96 -- a sixth more
+        // recomputed columns cost more than the unaligned stores (S = 10:
+        // 0.155 vs 0.169 ms per step, profiles/r04/ab_lp10.log)
+        const bool ow16 = knob("LBM_STREAM_OW16", ((tolerance && S <= 8) || S <= 5) ? 1 : 0) != 0;
         auto ow_of = [&](int rx) {
             const int n = ((rx - S) & 1) ? 126 - 2 * S : 128 - 2 * S;
             return ow16 ? n / 16 * 16 : n;
@@ -872,14 +875,14 @@ struct lbm_handle {
         // every sub-domain at least S cells (2S across a decomposed dimension)
         // launch form: the tolerance collision has forms 0 and 4 only
         if (tolerance) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
-        // the v3 kernel takes up to 6 steps per launch, 8 in the tolerance LP form
-        const int s_max = tolerance ? 8 : 6;
+        // the v3 kernel takes up to 6 steps per launch, 10 in the tolerance LP form
+        const int s_max = tolerance ? 10 : 6;
         const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch
                                                : std::min(tolerance ? tol_s : stream_s, s_max);
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max) +
-                                                 (tolerance ? "" : " (up to 8 with LBM_FLAG_TOLERANCE)"));
-        // the LP form exists for S = 6 (bitwise) and 6..8 (tolerance); S = 7, 8 have only it
+                                                 (tolerance ? "" : " (up to 10 with LBM_FLAG_TOLERANCE)"));
+        // the LP form exists for S = 6 (bitwise) and 6..10 (tolerance); S > 6 have only it
         if (S > 6) stream_cfg = 4;
         if (!s2d_form_ok(S, stream_cfg, tolerance)) stream_cfg = 0;
         bool can_stream = fused && S >= 2 && S <= s_max, big = true;
@@ -1532,6 +1535,13 @@ struct lbm_handle {
         }
     }
 
+    // launch form of a fused remainder launch of `steps` < spl steps: the
+    // engine's form where it has that depth, else the shallowest that does
+    int rem_form(int steps) const {
+        if (s2d_form_ok(steps, stream_cfg, tolerance)) return stream_cfg;
+        return steps > 6 ? 4 : 0;
+    }
+
     // Interior (reducing) or boundary launch of sub-domain s reading parity
     // `cur`: one fused launch (spl steps, WG halo) or one step (W1 halo).
     // steps > 0 (single sub-domain stream engines): a remainder launch of that
@@ -1541,9 +1551,7 @@ struct lbm_handle {
             const int n = interior ? s.n3_int : s.n3_bnd;
             if (n <= 0) return hipSuccess;
             const StreamArgs &a = interior ? s.a3_int[cur] : s.a3_bnd[cur];
-            if (steps > 0 && steps != spl)
-                return launch_stream2d(a, n, steps, interior, s2d_form_ok(steps, stream_cfg, tolerance) ? stream_cfg : 0,
-                                       tolerance, st);
+            if (steps > 0 && steps != spl) return launch_stream2d(a, n, steps, interior, rem_form(steps), tolerance, st);
             return launch_stream2d(a, n, spl, interior, stream_cfg, tolerance, st);
         }
         if (fused_launch) {

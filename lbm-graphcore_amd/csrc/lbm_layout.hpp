@@ -34,7 +34,7 @@ namespace lbm {
 
 constexpr int Q = 9;
 constexpr int XOFF = 4;   // interior column 0 offset inside a plane row
-constexpr int MAX_GR = 8;  // widest ghost ring (rows/columns) any kernel needs (stream kernel: S <= 8, tolerance)
+constexpr int MAX_GR = 10;  // widest ghost ring (rows/columns) any kernel needs (stream kernel: S <= 10, tolerance)
 // smallest interior column offset: an odd-S strip reads S + 1 columns left of
 // column 0 (float2 alignment), and rows must stay 16-B aligned
 constexpr int MIN_XOFF = (MAX_GR + 2 + 3) / 4 * 4;

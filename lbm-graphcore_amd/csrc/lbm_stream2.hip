@@ -150,7 +150,7 @@ __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2
 // SIMD, the bitwise form S = 6.
 template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL, bool LP>
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j,
-                                             const TolK &tk, f2 *lpl) {
+                                             const TolK &tk, f2 *lpl, float *lps) {
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
     // (LP forms issue row j+1's loads later, at level 2: see below)
     if (PD == 1 && !LP) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
@@ -175,26 +175,21 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         const int y = j - L;
         if constexpr (LP && PD == 1) {
             // LP forms: row j+1 is loaded once level 1 has consumed row j, into
-            // registers that are free by then -- one 18-VGPR row buffer
-            // instead of two; levels 2..S (>= 4 levels) cover the latency
+            // the row buffer itself (cur holds row j by then) -- one 18-VGPR
+            // row buffer; levels 2..S (>= 5 levels) cover the latency
             if (L == 2) {
-                stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
+                stream2d_load<PD, OBST>(a, g, j + 1, st.v[0], st.ob[0]);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
         // pulled populations of row y (level L-1 values; x +- 1 by DPP)
         f2 s[Q];
         if constexpr (LP) {
-            f2 *slot = lpl + b * 3 * 64;
-            s[2] = slot[0];
-            s[5] = slot[64];
-            s[6] = slot[128];
-            slot[0] = st.p2[0][b];
-            slot[64] = st.p5[0][b];
-            slot[128] = st.p6[0][b];
-            st.p2[0][b] = cur[2];
-            st.p5[0][b] = left2(cur[5]);
-            st.p6[0][b] = right2(cur[6]);
+            // LP: the registers hold row y-1 of planes 2, 5, 6 (the older row),
+            // the LDS slot row y; both move on after the collision (below)
+            s[2] = st.p2[0][b];
+            s[5] = st.p5[0][b];
+            s[6] = st.p6[0][b];
         } else {
             s[2] = st.p2[PAR][b];
             s[5] = st.p5[PAR][b];
@@ -209,10 +204,19 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         s[4] = cur[4];
         s[7] = right2(cur[7]);
         s[8] = left2(cur[8]);
-        st.c0[b] = cur[0];
-        st.c1[b] = left2(cur[1]);
-        st.c3[b] = right2(cur[3]);
-        if (GUARD && j < g.j0 + 2 * L) continue;  // inputs of this row were never loaded: result unused
+        if constexpr (!LP) {
+            st.c0[b] = cur[0];
+            st.c1[b] = left2(cur[1]);
+            st.c3[b] = right2(cur[3]);
+        }
+        // inputs of this row were never loaded: the result is unused.  The LP
+        // forms skip only the collision (the level's inputs still pass
+        // through, never reaching a store or a sum: rowlive) -- skipping the
+        // whole level makes the compiler hold a second copy of the level state
+        // in the tolerance forms (S = 7: 234 vs 202 VGPRs, S = 10: 35 spilled
+        // vs 254)
+        const bool cold = GUARD && j < g.j0 + 2 * L;
+        if (!LP && cold) continue;
 
         f2 o[Q];
         const bool oa = OBST && ((st.oba >> L) & 1u), ob = OBST && ((st.obb >> L) & 1u);
@@ -220,16 +224,40 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         int gy = a.gy0 + y;
         gy = gy < 0 ? gy + a.ny : (gy >= a.ny ? gy - a.ny : gy);
         f2 usq;
-        if constexpr (TOL)
+        if (LP && cold) {
+#pragma unroll
+            for (int k = 0; k < Q; ++k) o[k] = s[k];
+            usq = s[0];
+        } else if constexpr (TOL) {
             usq = collide2t(s, o, oa, ob, any_obst, gy == a.accel_g, tk, a.w1, a.w2);
-        else
+        } else {
             usq = collide2u(s, o, oa, ob, any_obst, gy == a.accel_g, a.omega, a.omo, a.w1, a.w2);
+        }
+        if constexpr (LP) {
+            // the level state moves on once the collision has consumed the old
+            // rows, so the new values can take the old ones' registers (updated
+            // before the collision they needed a register each plus a copy:
+            // ~5 v_mov_b64 per level and row): planes 2, 5, 6 of row y from the
+            // LDS slot into the registers, row y+1 into the slot (read before
+            // write: one wave's LDS operations stay in order), planes 0, 1, 3
+            // of row y+1
+            f2 *slot = lpl + b * 3 * 64;
+            st.p2[0][b] = slot[0];
+            st.p5[0][b] = slot[64];
+            st.p6[0][b] = slot[128];
+            slot[0] = cur[2];
+            slot[64] = left2(cur[5]);
+            slot[128] = right2(cur[6]);
+            st.c0[b] = cur[0];
+            st.c1[b] = left2(cur[1]);
+            st.c3[b] = right2(cur[3]);
+        }
         const bool rowlive = (!GUARD || y >= g.yo0) && (L == S || y < g.yo1);
         if (rowlive) {
             const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
             const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
             if constexpr (LP)
-                lpl[(3 * S + b) * 64].x += ua + ub;  // LP: the per-level |u| sums in LDS, not VGPRs
+                lps[b * 64] += ua + ub;  // LP: the per-level |u| sums in LDS, not VGPRs
             else
                 st.tot[b] += ua + ub;
         }
@@ -301,8 +329,15 @@ __device__ __forceinline__ Stream2Geo stream2d_geo(const StreamArgs &a, int t, i
 }
 
 // One work unit (strip x segment t) of the launch; accumulates |u| per level into st.tot.
+// LP forms walk the rows one per iteration (the non-LP forms two, with the
+// rows y-1 / y of planes 2, 5, 6 in parity-alternating registers): unrolling
+// by two lets the compiler give every level-state value a register per
+// parity instead of one register and a copy, which costs 6-8 VGPRs per level
+// (S = 10: 253 VGPRs without spills one row per iteration; 256 + 221 spilled
+// two rows per iteration).
 template <int S, int PD, bool NT, bool OBST, bool TOL, bool LP>
-__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st, f2 *lpl) {
+__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st, f2 *lpl,
+                                              float *lps) {
     const Stream2Geo g = stream2d_geo<S>(a, t, lane);
     const TolK tk{a.omo, a.tc0, a.tc1, a.tc2};
     if constexpr (LP) {
@@ -321,17 +356,24 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     if (PD == 2) stream2d_load<PD, OBST>(a, g, g.j0 + 1, st.v[1], st.ob[1]);
     // warm-up: rows j0 .. j0+2S-1 (level L valid from j0+2L); jlast >= j0+2S
     int j = g.j0;
+    if constexpr (LP) {
 #pragma unroll 1
-    for (int i = 0; i < S; ++i, j += 2) {
-        stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
-        stream2d_row<S, 1, true, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl);
-    }
+        for (int i = 0; i < 2 * S; ++i, ++j) stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
 #pragma unroll 1
-    for (; j + 1 <= g.jlast; j += 2) {
-        stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
-        stream2d_row<S, 1, false, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl);
+        for (; j <= g.jlast; ++j) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
+    } else {
+#pragma unroll 1
+        for (int i = 0; i < S; ++i, j += 2) {
+            stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
+            stream2d_row<S, 1, true, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl, lps);
+        }
+#pragma unroll 1
+        for (; j + 1 <= g.jlast; j += 2) {
+            stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
+            stream2d_row<S, 1, false, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl, lps);
+        }
+        if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
     }
-    if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
 }
 
 // |u| partials of one work unit, one per level (= time step of the launch)
@@ -366,17 +408,20 @@ __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, 
 template <int S, bool kReduce, int W, bool NT, bool TOL = false, bool LP = false>
 __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     __shared__ float lds[W];
-    __shared__ f2 lds_p[LP ? W * 4 * S * 64 : 1];  // LP: [wave] {[S][3][64] rows, [S][64] |u| sums}
+    __shared__ f2 lds_p[LP ? W * 3 * S * 64 : 1];   // LP: [wave][S][3][64] older rows of planes 2, 5, 6
+    __shared__ float lds_u[LP ? W * S * 64 : 1];    // LP: [wave][S][64] |u| sums
+    // (S = 10: 17.5 KB per one-wave workgroup, so eight fit a CU's 160 KB)
     if (kReduce && blockIdx.x == 0) reduce_pending_n<64 * W>(a.ctl, a.partials_prev, a.av_local, lds);
 
     const int lane = threadIdx.x & 63;
     Stream2State<S> st;
 #pragma unroll
     for (int l = 0; l < S; ++l) st.tot[l] = 0.f;
-    f2 *const lpl = lds_p + (LP ? (threadIdx.x >> 6) * 4 * S * 64 : 0) + lane;
+    f2 *const lpl = lds_p + (LP ? (threadIdx.x >> 6) * 3 * S * 64 : 0) + lane;
+    float *const lps = lds_u + (LP ? (threadIdx.x >> 6) * S * 64 : 0) + lane;
     if constexpr (LP) {
 #pragma unroll
-        for (int l = 0; l < S; ++l) lpl[(3 * S + l) * 64] = mk2(0.f);
+        for (int l = 0; l < S; ++l) lps[l * 64] = 0.f;
     }
     // wave-uniform: keeps the unit geometry and the row loop in scalar registers
     const int slot = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6));
@@ -391,13 +436,13 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
         // read no obstacle cell run the select-free copy of the unit loop
         typedef const __attribute__((address_space(4))) uint8_t CU8;
         if (a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0)
-            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lpl);
+            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lpl, lps);
         else
-            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lpl);
+            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lpl, lps);
     }
     if constexpr (LP) {
 #pragma unroll
-        for (int l = 0; l < S; ++l) st.tot[l] = lpl[(3 * S + l) * 64].x;
+        for (int l = 0; l < S; ++l) st.tot[l] = lps[l * 64];
     }
     if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
@@ -435,6 +480,8 @@ hipError_t stream2d_unit_flags(const StreamArgs &a, int steps, uint8_t *uobst, h
         case 6: hipLaunchKernelGGL(stream2d_flags<6>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 7: hipLaunchKernelGGL(stream2d_flags<7>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         case 8: hipLaunchKernelGGL(stream2d_flags<8>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 9: hipLaunchKernelGGL(stream2d_flags<9>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
+        case 10: hipLaunchKernelGGL(stream2d_flags<10>, dim3(a.total), dim3(64), 0, s, a, uobst); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -461,7 +508,7 @@ static const void *s2d_fn() {
 //   forms measure equal, profiles/r03/ab_forms_s5_s6.log; tolerance S = 6..8).
 // tol: the LBM_FLAG_TOLERANCE collision (collide2t) in forms 0 and 4.
 bool s2d_form_ok(int steps, int cfg, bool tol) {
-    if (cfg == 4) return steps == 6 || (tol && (steps == 7 || steps == 8));
+    if (cfg == 4) return steps == 6 || (tol && steps >= 7 && steps <= 10);
     if (cfg == 0) return steps >= 2 && steps <= 6;
     if (cfg == 3) return !tol && steps >= 2 && steps <= 6;
     return false;
@@ -476,6 +523,8 @@ hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
         switch (steps) {
             case 7: fn = s2d_fn<7, true, true>(); break;
             case 8: fn = s2d_fn<8, true, true>(); break;
+            case 9: fn = s2d_fn<9, true, true>(); break;
+            case 10: fn = s2d_fn<10, true, true>(); break;
             default: fn = tol ? s2d_fn<6, true, true>() : s2d_fn<6, false, true>(); break;
         }
     } else {  // cfg 3 has the registers of cfg 0
@@ -498,6 +547,8 @@ hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduc
             case 13: launch_s2d<6, false, true, true>(a, units, reduce, s); break;
             case 15: launch_s2d<7, false, true, true>(a, units, reduce, s); break;
             case 17: launch_s2d<8, false, true, true>(a, units, reduce, s); break;
+            case 19: launch_s2d<9, false, true, true>(a, units, reduce, s); break;
+            case 21: launch_s2d<10, false, true, true>(a, units, reduce, s); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

@@ -36,8 +36,8 @@ void usage(const char *exe) {
               << "      --runs arg       timed re-runs after the first (default: 5)\n"
               << "      --kernel arg     auto, resident, stream, step2, vec4, scalar or pipeline (default: auto; vec4/scalar = one\n"
               << "                       step per launch; pipeline = unfused per-stage kernels)\n"
-              << "      --spl arg        stream kernel: time steps per launch, 2..6, 2..8 with --tolerance (default:\n"
-              << "                       library choice, 6; 7 with --tolerance)\n"
+              << "      --spl arg        stream kernel: time steps per launch, 2..6, 2..10 with --tolerance (default:\n"
+              << "                       library choice, 6; 10 with --tolerance)\n"
               << "      --tolerance      fp32 tolerance-mode collision (LBM_FLAG_TOLERANCE: one reciprocal of rho per\n"
               << "                       cell; not bit-identical to the reference, within the tolerance lbm_hip.h states)\n"
               << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n"

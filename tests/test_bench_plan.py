@@ -14,14 +14,14 @@ import bench  # noqa: E402
 
 def test_pick_spl_driver_and_default_runs():
     assert bench.pick_spl(20, 0, "bitwise") == 5        # 4 x 5
-    assert bench.pick_spl(20, 0, "tolerance") == 7      # 7 + 7 + 6
+    assert bench.pick_spl(20, 0, "tolerance") == 10     # 2 x 10
     assert bench.pick_spl(1000, 0, "bitwise") == 6      # 166 x 6 + 4
-    assert bench.pick_spl(1000, 0, "tolerance") == 7    # 142 x 7 + 6
+    assert bench.pick_spl(1000, 0, "tolerance") == 10   # 100 x 10
     assert bench.pick_spl(20, 4, "tolerance") == 4      # the caller's choice wins
 
 
 def test_pick_spl_every_step_count_is_valid():
-    for numerics, smax in (("bitwise", 6), ("tolerance", 8)):
+    for numerics, smax in (("bitwise", 6), ("tolerance", 10)):
         for steps in range(0, 200):
             S = bench.pick_spl(steps, 0, numerics)
             assert 2 <= S <= smax

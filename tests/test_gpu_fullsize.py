@@ -79,7 +79,8 @@ def test_16384_eight_subdomains_bitwise(gpu_lib, single_16384, grid):
     assert np.isfinite(d14[0][::251, ::241]).all()
 
 
-TOL_STEPS = (9, 13)  # S = 7: 7 + a fused 2-step remainder, then 7 + a fused 6-step remainder
+TOL_STEPS = (9, 13)  # S = 10: one fused 9-step launch, then 10 + a fused 3-step remainder
+TOL_STATS = [(1, 0), (2, 0)]
 
 
 @pytest.fixture(scope="module")
@@ -88,14 +89,14 @@ def single_16384_tolerance(gpu_lib):
     obst = _obstacles_2d(N2)
     kernel, rects, s9, s22, stats = _run_2d(gpu_lib, p, obst, steps=TOL_STEPS, flags=gpu_lib.FLAG_TOLERANCE)
     assert kernel == "stream" and len(rects) == 1
-    assert stats == [(2, 0), (2, 0)]
+    assert stats == TOL_STATS
     assert np.isfinite(s22[0][::251, ::241]).all()
     return p, obst, s9, s22
 
 
 @pytest.mark.parametrize("grid", [(2, 4), (8, 1)], ids=["2x4-reference-rule", "8x1-slabs"])
 def test_16384_eight_subdomains_tolerance_bitwise(gpu_lib, single_16384_tolerance, grid):
-    """The tolerance plan bench.py publishes for config 4 (S = 7 launches and
+    """The tolerance plan bench.py publishes for config 4 (S = 10 launches and
     fused remainders), decomposed as the 8-GPU runs decompose it, against its
     single-domain run: the tolerance collision is the same per-cell arithmetic
     everywhere, so the lattices must be bitwise equal."""
@@ -104,10 +105,10 @@ def test_16384_eight_subdomains_tolerance_bitwise(gpu_lib, single_16384_toleranc
     kernel, rects, d9, d22, stats = _run_2d(gpu_lib, p, obst, steps=TOL_STEPS, flags=gpu_lib.FLAG_TOLERANCE, **kw)
     assert kernel == "stream" and len(rects) == 8
     assert {(r[2], r[3]) for r in rects} == {(N2 // grid[1], N2 // grid[0])}
-    assert stats == [(2, 0), (2, 0)]
-    assert np.array_equal(d9[0], s9[0]), "after 9 steps (7 + fused 2)"
+    assert stats == TOL_STATS
+    assert np.array_equal(d9[0], s9[0]), "after 9 steps (one fused 9-step launch)"
     np.testing.assert_allclose(d9[1], s9[1], rtol=1e-4)
-    assert np.array_equal(d22[0], s22[0]), "after 13 more (7 + fused 6)"
+    assert np.array_equal(d22[0], s22[0]), "after 13 more (10 + fused 3)"
     np.testing.assert_allclose(d22[1], s22[1], rtol=1e-4)
 
 

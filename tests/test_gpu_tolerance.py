@@ -97,29 +97,30 @@ def test_tolerance_8192_vs_oracle(gpu_lib):
 def test_tolerance_16384_vs_oracle(gpu_lib):
     """BASELINE config 4's grid in the mode bench.py publishes for it
     (aux.config4_16384x16384): single domain, tolerance collision, default
-    S = 7, placement probe on.  9 steps = one 7-step launch + ONE fused 2-step
-    remainder launch; one lattice holds 2.4e9 floats (over 2^31), so every
-    index of the LP form and of the remainder launch must be 64-bit.  Every
-    population within TOL_POP of the oracle."""
+    S = 10, placement probe on.  13 steps = one 10-step launch + ONE fused
+    3-step remainder launch; one lattice holds 2.4e9 floats (over 2^31), so
+    every index of the LP form and of the remainder launch must be 64-bit.
+    Every population within TOL_POP of the oracle."""
     n = 16384
-    p = lio.Params(n, n, 9, 10, 0.1, 0.005, 1.85)
+    steps = 13
+    p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
     obst = np.zeros((n, n), np.uint8)
     obst[0, :] = obst[-1, :] = 1
     obst[:, 0] = obst[:, -1] = 1
     obst[:, n // 3] = 1
     with gpu_lib.Engine(p, obst, flags=gpu_lib.FLAG_TOLERANCE) as e:
         assert e.kernel_in_use() == "stream" and e.numerics() == "tolerance"
-        assert e.steps_per_launch() == 7
+        assert e.steps_per_launch() == 10
         e.init_equilibrium()
-        e.run_steps(9, accelerate_first=True)
+        e.run_steps(steps, accelerate_first=True)
         assert e.run_stats() == (2, 0)
-        cells, av = e.store(n_av=9)
+        cells, av = e.store(n_av=steps)
     assert np.isfinite(av).all()
-    ref, ref_av = oracle.run_mt(p, obst, 9, 16, lio.init_cells(p))
+    ref, ref_av = oracle.run_mt(p, obst, steps, 16, lio.init_cells(p))
     dev = _rel(cells, ref)
     del cells, ref
     dav = float(np.max(np.abs(av - ref_av) / np.abs(ref_av)))
-    print(f"16384^2, 9 steps (7 + fused 2): populations max relative deviation {dev:.3e}, av_vels {dav:.3e}")
+    print(f"16384^2, 13 steps (10 + fused 3): populations max relative deviation {dev:.3e}, av_vels {dav:.3e}")
     assert dev < TOL_POP
     assert dav < 5e-3  # 268M-term sequential fp32 sums in the oracle (bitwise mode: 5e-3 too)
 
@@ -186,8 +187,8 @@ def test_tolerance_resident_tiles_vs_stream(gpu_lib, th, monkeypatch):
 
 @pytest.mark.parametrize("steps", [24, 30])
 def test_tolerance_steps_per_launch_invariant(gpu_lib, steps):
-    """Tolerance launches of S = 2..8 steps (plain forms up to 6, the LP form
-    at 6..8; fused remainder launches of 2..7 steps) run the same per-cell
+    """Tolerance launches of S = 2..10 steps (plain forms up to 6, the LP form
+    at 6..10; fused remainder launches of 2..9 steps) run the same per-cell
     arithmetic: the lattice does not depend on S, single domain and 2x2
     loop-back alike, and stays within TOL_POP of the oracle.  24 and 30 steps
     leave no one-step (bitwise-collision) remainder for any S."""
@@ -198,7 +199,7 @@ def test_tolerance_steps_per_launch_invariant(gpu_lib, steps):
     cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((260, 300, 9)))).astype(np.float32)
     ref, ref_av = oracle.run(p, obst, steps, cells0)
     out = []
-    for S in range(2, 9):
+    for S in range(2, 11):
         for kw in (dict(), dict(parts=4, grid=(2, 2))):
             with gpu_lib.Engine(p, obst, devices=[0], **_tol_kw(gpu_lib, steps_per_launch=S, **kw)) as e:
                 assert e.steps_per_launch() == S and e.numerics() == "tolerance"
