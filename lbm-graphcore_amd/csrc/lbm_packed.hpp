@@ -171,22 +171,27 @@ __device__ __forceinline__ f2 collide2u(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
 }
 
 // LBM_FLAG_TOLERANCE collision: the same BGK step as collide2u, reassociated
-// for fewer VALU instructions (61 packed + 2 v_rcp_f32 per cell pair against
+// for fewer VALU instructions (56 packed + 2 v_rcp_f32 per cell pair against
 // 95 packed + 63 scalar in the bitwise form).  Not bitwise equal to
 // LastChance.cpp:226-262 -- within the tolerance lbm_hip.h states:
 //   * 1/rho once per cell (v_rcp_f32, 1 ulp, plus one Newton step), shared by
-//     u_x and u_y, instead of two correctly rounded divisions;
+//     u_x and u_y, instead of two correctly rounded divisions; the velocities
+//     are carried scaled, v = 3u = (m / rho) * 3;
 //   * rho/9 * omega and rho/36 * omega as rho * (omega/9), rho * (omega/36);
-//   * out_k = s_k (1 - omega) + ld ((+-4.5 v)(2/3 +- v) + c) written as
-//     fma(s_k, 1 - omega, P +- Q) with P = ld (4.5 v^2 + c), Q = 3 ld v,
-//     shared by each pair of opposite speeds;
+//   * out_k = s_k (1 - omega) + ld ((+-4.5 u)(2/3 +- u) + c) written as
+//     fma(+-ld, v, fma(s_k, 1 - omega, P)) with P = ld (v^2 / 2 + c) shared by
+//     each pair of opposite speeds and c = 1 - (vx^2 + vy^2) / 6 (the
+//     3 ld u term rides in the outer fma instead of its own multiply);
 //   * the folded acceleration only on the accelerated row (adding 0 * w
 //     elsewhere changes nothing but the sign of a zero).
+// Returns vx^2 + vy^2 = 9 |u|^2: the callers sum its square root and scale
+// the sum by TOL_USQ_ROOT = 1/3 once, where the |u| partials are written.
 // k = {1 - omega, 4 omega / 9, omega / 9, omega / 36}: wave-uniform scalars
 // (kernel arguments, formed on the host), so they live in SGPRs, not VGPRs.
 struct TolK {
     float omo, c0, c1, c2;
 };
+constexpr float TOL_USQ_ROOT = 1.00f / 3.00f;
 __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, bool accrow,
                                         const TolK &k, float w1, float w2) {
     const f2 a = s[1] + s[5] + s[8], b = s[3] + s[6] + s[7];
@@ -194,37 +199,37 @@ __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
     const f2 rho = (s[0] + s[2] + s[4]) + (a + b);
     f2 r = f2{__builtin_amdgcn_rcpf(rho.x), __builtin_amdgcn_rcpf(rho.y)};
     r = fma2(r, fma2(-rho, r, mk2(1.00f)), r);  // one Newton step: ~0.5 ulp
-    const f2 ux = (a - b) * r, uy = (c - d) * r;
-    const f2 uxx = ux * ux, uyy = uy * uy;
-    const f2 usq = uxx + uyy;
-    const f2 csq = fma2(usq, mk2(-1.50f), mk2(1.00f));
+    const f2 r3 = r * mk2(3.00f);
+    const f2 vx = (a - b) * r3, vy = (c - d) * r3;  // 3 u
+    const f2 hx = vx * vx, hy = vy * vy;
+    const f2 h = hx + hy;                             // 9 |u|^2
+    const f2 csq = fma2(h, mk2(-1.00f / 6.00f), mk2(1.00f));
     const f2 ld1 = rho * mk2(k.c1), ld2 = rho * mk2(k.c2);
     const f2 omo = mk2(k.omo);
-    const f2 l3 = ld1 * mk2(3.00f), m3 = ld2 * mk2(3.00f);
-    const f2 c45 = mk2(4.50f);
+    const f2 half = mk2(0.50f);
     f2 cc[Q];
     cc[0] = fma2(s[0], omo, (rho * mk2(k.c0)) * csq);
     {
-        const f2 p = ld1 * fma2(uxx, c45, csq), q = l3 * ux;
-        cc[1] = fma2(s[1], omo, p + q);
-        cc[3] = fma2(s[3], omo, p - q);
+        const f2 p = ld1 * fma2(hx, half, csq);
+        cc[1] = fma2(ld1, vx, fma2(s[1], omo, p));
+        cc[3] = fma2(-ld1, vx, fma2(s[3], omo, p));
     }
     {
-        const f2 p = ld1 * fma2(uyy, c45, csq), q = l3 * uy;
-        cc[2] = fma2(s[2], omo, p + q);
-        cc[4] = fma2(s[4], omo, p - q);
+        const f2 p = ld1 * fma2(hy, half, csq);
+        cc[2] = fma2(ld1, vy, fma2(s[2], omo, p));
+        cc[4] = fma2(-ld1, vy, fma2(s[4], omo, p));
     }
     {
-        const f2 us = ux + uy;
-        const f2 p = ld2 * fma2(us * us, c45, csq), q = m3 * us;
-        cc[5] = fma2(s[5], omo, p + q);
-        cc[7] = fma2(s[7], omo, p - q);
+        const f2 ws = vx + vy;
+        const f2 p = ld2 * fma2(ws * ws, half, csq);
+        cc[5] = fma2(ld2, ws, fma2(s[5], omo, p));
+        cc[7] = fma2(-ld2, ws, fma2(s[7], omo, p));
     }
     {
-        const f2 ud = uy - ux;
-        const f2 p = ld2 * fma2(ud * ud, c45, csq), q = m3 * ud;
-        cc[6] = fma2(s[6], omo, p + q);
-        cc[8] = fma2(s[8], omo, p - q);
+        const f2 wd = vy - vx;
+        const f2 p = ld2 * fma2(wd * wd, half, csq);
+        cc[6] = fma2(ld2, wd, fma2(s[6], omo, p));
+        cc[8] = fma2(-ld2, wd, fma2(s[8], omo, p));
     }
     if (accrow) {
         // a real (wave-uniform) branch: without this barrier to speculation
@@ -242,12 +247,12 @@ __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
     if (!any_obst) {
 #pragma unroll
         for (int i = 0; i < Q; ++i) o[i] = cc[i];
-        return usq;
+        return h;
     }
     constexpr int OPP[Q] = {0, 3, 4, 1, 2, 7, 8, 5, 6};
 #pragma unroll
     for (int i = 0; i < Q; ++i) o[i] = f2{oa ? s[OPP[i]].x : cc[i].x, ob ? s[OPP[i]].y : cc[i].y};
-    return usq;
+    return h;
 }
 
 }  // namespace lbm

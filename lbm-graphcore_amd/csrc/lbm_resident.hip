@@ -558,6 +558,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         if (poll_it == MAXIT - 1) poll_ring();
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) tot += __shfl_down(tot, off, 64);
+        if (TOL) tot *= TOL_USQ_ROOT;  // collide2t returns 9 |u|^2
         if (lane == 0) wsum[wv] = tot;
         if (tr) a.trace[t * 5 + 2] = (long long)wall_clock64();
         if (tr) a.trace[t * 5 + 3] = (long long)wall_clock64();

@@ -377,13 +377,15 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
 }
 
 // |u| partials of one work unit, one per level (= time step of the launch)
-template <int S>
+// (TOL: the sums are of sqrt(9 |u|^2), collide2t; scaled by 1/3 here, once)
+template <int S, bool TOL>
 __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, int lane, Stream2State<S> &st) {
 #pragma unroll
     for (int l = 0; l < S; ++l) {
         float sum = st.tot[l];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
+        if (TOL) sum *= TOL_USQ_ROOT;
         if (lane == 0) a.partials_out[(long long)l * a.stride + idx] = sum;
         st.tot[l] = 0.f;
     }
@@ -444,7 +446,7 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
 #pragma unroll
         for (int l = 0; l < S; ++l) st.tot[l] = lps[l * 64];
     }
-    if (t < max(a.total, 1)) stream2d_partials<S>(a, t, lane, st);
+    if (t < max(a.total, 1)) stream2d_partials<S, TOL>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         a.trace[2 * (long long)t] = t_start;
