@@ -223,9 +223,11 @@ __device__ __forceinline__ float cell3d(const float (&s)[Q3], float (&o)[Q3], bo
 }
 
 // LBM_FLAG_TOLERANCE form of cell3d (the 2-D collide2t's reassociation in
-// 3-D): one reciprocal of rho (v_rcp_f32 + a Newton step) for u_x, u_y, u_z,
-// rho * (omega / 3 | 18 | 36), out_k = fma(s_k, 1 - omega, P +- Q) per pair of
-// opposite speeds with P = ld (4.5 v^2 + c), Q = 3 ld v.  Not bitwise equal to
+// 3-D): one reciprocal of rho (v_rcp_f32 + a Newton step) for the velocity,
+// carried scaled (v = 3u), rho * (omega / 3 | 18 | 36), and per pair of
+// opposite speeds out_k = fma(s_k, 1 - omega, P) +- Q with P = ld (v^2 / 2 +
+// c), c = 1 - |v|^2 / 6, Q = ld v (+ the body-force weight of the pair, which
+// enters the two outputs with opposite signs).  Not bitwise equal to
 // oracle/lbm_oracle3d.c; checked against it within a stated tolerance
 // (tests/test_d3q19.py test_d3q19_tolerance_*).  k = {1 - omega, omega/3,
 // omega/18, omega/36}.
@@ -255,37 +257,33 @@ __device__ __forceinline__ float cell3dt(const float (&s)[Q3], float (&o)[Q3], b
     const float rho = ((s[0] + (s[3] + s[4])) + (ax + bx)) + ((s[9] + s[12] + s[13]) + (s[14] + s[17] + s[18]));
     float r = __builtin_amdgcn_rcpf(rho);
     r = __builtin_fmaf(r, __builtin_fmaf(-rho, r, 1.00f), r);
-    const float ux = (ax - bx) * r, uy = (ay - by) * r, uz = (az - bz) * r;
-    const float usq = __builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz));
-    const float c = __builtin_fmaf(usq, -1.50f, 1.00f);
+    const float r3 = r * 3.00f;
+    const float vx = (ax - bx) * r3, vy = (ay - by) * r3, vz = (az - bz) * r3;  // 3 u
+    const float h = __builtin_fmaf(vx, vx, __builtin_fmaf(vy, vy, vz * vz));   // 9 |u|^2
+    const float c = __builtin_fmaf(h, -1.00f / 6.00f, 1.00f);
     const float ld1 = rho * k1, ld2 = rho * k2;
-    const float l3 = ld1 * 3.00f, m3 = ld2 * 3.00f;
     o[0] = __builtin_fmaf(s[0], omo, (rho * k0) * c);
-    auto pair = [&](int kp, int km, float v, float ld, float ld3) {
-        const float p = ld * __builtin_fmaf(v * v, 4.50f, c), q = ld3 * v;
-        o[kp] = __builtin_fmaf(s[kp], omo, p + q);
-        o[km] = __builtin_fmaf(s[km], omo, p - q);
+    // q: the pair's +- term, w: its body-force weight (+w on kp, -w on km)
+    auto pair = [&](int kp, int km, float v, float ld, float w) {
+        const float p = ld * __builtin_fmaf(v * v, 0.50f, c), q = __builtin_fmaf(ld, v, w);
+        o[kp] = __builtin_fmaf(s[kp], omo, p) + q;
+        o[km] = __builtin_fmaf(s[km], omo, p) - q;
     };
-    pair(1, 2, ux, ld1, l3);
-    pair(3, 4, uy, ld1, l3);
-    pair(9, 14, uz, ld1, l3);
-    pair(5, 6, ux + uy, ld2, m3);
-    pair(7, 8, ux - uy, ld2, m3);
-    pair(10, 15, ux + uz, ld2, m3);
-    pair(11, 16, uz - ux, ld2, m3);
-    pair(12, 17, uy + uz, ld2, m3);
-    pair(13, 18, uz - uy, ld2, m3);
-    o[1] = o[1] + w1;
-    o[2] = o[2] - w1;
-    o[5] = o[5] + w2;
-    o[6] = o[6] - w2;
-    o[7] = o[7] + w2;
-    o[8] = o[8] - w2;
-    o[10] = o[10] + w2;
-    o[11] = o[11] - w2;
-    o[15] = o[15] - w2;
-    o[16] = o[16] + w2;
-    return __builtin_amdgcn_sqrtf(usq);
+    auto pair0 = [&](int kp, int km, float v, float ld) {  // no body force on this pair
+        const float p = ld * __builtin_fmaf(v * v, 0.50f, c);
+        o[kp] = __builtin_fmaf(ld, v, __builtin_fmaf(s[kp], omo, p));
+        o[km] = __builtin_fmaf(-ld, v, __builtin_fmaf(s[km], omo, p));
+    };
+    pair(1, 2, vx, ld1, w1);
+    pair0(3, 4, vy, ld1);
+    pair0(9, 14, vz, ld1);
+    pair(5, 6, vx + vy, ld2, w2);
+    pair(7, 8, vx - vy, ld2, w2);
+    pair(10, 15, vx + vz, ld2, w2);
+    pair(11, 16, vz - vx, ld2, -w2);
+    pair0(12, 17, vy + vz, ld2);
+    pair0(13, 18, vz - vy, ld2);
+    return __builtin_amdgcn_sqrtf(h) * (1.00f / 3.00f);  // |u|, av_vels only
 }
 
 // Two cells per lane (a column pair, nx even): every load and store is a
@@ -823,6 +821,7 @@ struct lbm3d_handle {
     bool poison = false;  // LBM_POISON=1: fresh allocations filled with NaN bytes
     int probe_tries = 4;  // LBM3D_PLACEMENT_TRIES: lattice pairs the placement probe times (1 = off)
     long long probe_min_cells = 1LL << 26;  // LBM3D_PROBE_MIN_CELLS: smallest single slab probed
+    bool probe_tol = false;                  // LBM3D_PROBE_TOL=1: probe tolerance-mode engines too (A/B)
     bool probe_log = false;  // LBM_PLACEMENT_LOG: print the probe's per-pair times
     bool tolerance = false;  // LBM_FLAG_TOLERANCE: the two-step passes use cell3dt (not bitwise)
     std::vector<Slab> slabs;
@@ -881,6 +880,7 @@ struct lbm3d_handle {
         lattice_pad = knob("LBM_LATTICE_PAD");
         if (const char *t = knob("LBM3D_PLACEMENT_TRIES")) probe_tries = std::max(1, atoi(t));
         if (const char *m = knob("LBM3D_PROBE_MIN_CELLS")) probe_min_cells = std::max(0LL, atoll(m));
+        if (const char *pt = knob("LBM3D_PROBE_TOL")) probe_tol = atoi(pt) != 0;
         probe_log = knob("LBM_PLACEMENT_LOG") != nullptr;
         if (tolerance) {  // the tolerance pass exists for the default block only
             th = 12;
@@ -968,7 +968,7 @@ struct lbm3d_handle {
     // measured to follow the two-step pass's, so they skip the probe (and its
     // transient ~82 GB of candidate pairs at 512^3).
     void placement_probe() {
-        if (multi() || !use_two() || use_three() || slabs.size() != 1) return;
+        if (multi() || !use_two() || (use_three() && !probe_tol) || slabs.size() != 1) return;
         Slab &s = slabs[0];
         if ((long long)p.nx * p.ny * p.nz < probe_min_cells || s.f_joint) return;
         const size_t floats = (size_t)(s.nzs + 2 * GZ3) * PL;
