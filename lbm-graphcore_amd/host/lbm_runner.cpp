@@ -1,7 +1,7 @@
 // lbm_runner -- the reference's LbmRunner CLI (main/LbmRunner.cpp:11-147) on
 // top of the HIP engine's C ABI instead of a Poplar Engine.
 //
-//   lbm_runner --params P --obstacles O [-n N] [--device gpu|loopback] [-d] [--exe ignored]
+//   lbm_runner --params P --obstacles O [-n N] [--device gpu|loopback|cpu] [-d] [--exe ignored]
 //              [--runs 5] [--kernel auto|resident|stream|step2|vec4|scalar|pipeline] [--spl S] [--out-dir DIR]
 //
 // Flow (same program numbering as the reference):
@@ -12,14 +12,19 @@
 //   then `runs` more lbm_run calls timed by device events (≙ readTimer).
 // --device loopback places all N sub-domains on GPU 0 (the emulator analogue
 // of --device ipumodel: exercises the multi-GPU halo path on one device).
+// --device cpu runs the same fused step on the host's cores (lbm_cpu.hpp:
+// OpenMP rows, bitwise equal to the GPU engine's default numerics); -n and
+// the GPU-only options are ignored there.
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iomanip>
 #include <iostream>
+#include <memory>
 #include <string>
 #include <vector>
 
+#include "lbm_cpu.hpp"
 #include "lbm_host.hpp"
 
 namespace {
@@ -28,7 +33,7 @@ void usage(const char *exe) {
     std::cerr << exe << " - Runs the Lattice Boltzmann D2Q9-BGK engine on MI355X GPUs\n"
               << "Usage:\n  " << exe << " [OPTION...]\n\n"
               << "  -d, --debug          Print per-phase detail\n"
-              << "      --device arg     gpu or loopback (default: gpu)\n"
+              << "      --device arg     gpu, loopback or cpu (default: gpu)\n"
               << "  -n, --num-gpus arg   number of GPUs / sub-domains to use (default: 1)\n"
               << "      --exe arg        accepted for compatibility with the reference (ignored)\n"
               << "      --params arg     filename of parameters file\n"
@@ -43,6 +48,46 @@ void usage(const char *exe) {
               << "      --out-dir arg    directory for av_vels.dat / final_state.dat (default: .)\n"
               << "      --graph-steps arg  replay the step loop as hipGraphs of 2*arg launches (0 = library default, <0 = off)\n"
               << "      --dump-partitioning arg  write the sub-domain decomposition as JSON\n";
+}
+
+// --device cpu: the reference's program sequence on the host backend
+int run_cpu(const lbmhost::Params &params, const lbmhost::Obstacles &obstacles, const std::string &outDir, int runs) {
+    std::cout << "Running on the host CPU (" << lbmcpu::Engine::threads() << " threads)" << std::endl;
+    auto cells = lbmhost::initialiseCells(params);
+    std::vector<float> av_vels;
+    std::unique_ptr<lbmcpu::Engine> e;
+    lbmhost::timedStep("Creating engine and loading obstacles", [&]() {
+        e = std::make_unique<lbmcpu::Engine>((int)params.nx, (int)params.ny, params.density, params.accel,
+                                             params.omega, obstacles.data);
+    });
+    lbmhost::timedStep("Running copy to device step", [&]() { e->load(cells); });
+    double total_compute_time =
+        lbmhost::timedStep("Running LBM", [&]() { e->run((int)params.maxIters, av_vels); });
+    lbmhost::timedStep("Running copy to host step", [&]() { e->store(cells); });
+    lbmhost::timedStep("Writing output files ", [&]() {
+        lbmhost::writeAverageVelocities(outDir + "/av_vels.dat", av_vels);
+        lbmhost::writeResults(outDir + "/final_state.dat", params, obstacles, cells);
+    });
+    std::cout << "==done==" << std::endl;
+    std::cout << "Total compute time was \t" << std::right << std::setw(12) << std::setprecision(5)
+              << total_compute_time << "s" << std::endl;
+    const float lastAv = params.maxIters > 0 ? av_vels[params.maxIters - 1] : 0.f;
+    std::cout << "Reynolds number:  \t" << std::right << std::setw(12) << std::setprecision(12) << std::scientific
+              << lbmhost::reynoldsNumber(params, lastAv) << std::endl;
+    if (runs > 0) {
+        std::cout << "Now doing " << runs << " runs and averaging CPU timing:" << std::endl;
+        double secs = 0.0;
+        for (int r = 0; r < runs; ++r) {
+            e->load(cells);
+            secs += e->run((int)params.maxIters, av_vels);
+        }
+        const double avg = secs / runs;
+        std::cout << "Average CPU timing for program is: " << std::fixed << std::setprecision(5) << std::setw(12)
+                  << avg << "s" << std::endl;
+        std::cout << "MLUPS: " << std::fixed << std::setprecision(1)
+                  << (double)params.nx * params.ny * params.maxIters / avg / 1e6 << std::endl;
+    }
+    return EXIT_SUCCESS;
 }
 
 }  // namespace
@@ -110,7 +155,8 @@ int main(int argc, char *argv[]) {
             return EXIT_FAILURE;
         }
     }
-    if (paramsFile.empty() || obstaclesFile.empty() || numGpus < 1 || (device != "gpu" && device != "loopback")) {
+    if (paramsFile.empty() || obstaclesFile.empty() || numGpus < 1 ||
+        (device != "gpu" && device != "loopback" && device != "cpu")) {
         usage(argv[0]);
         return EXIT_FAILURE;
     }
@@ -153,6 +199,7 @@ int main(int argc, char *argv[]) {
         f << "\n]}\n";
         std::cout << "Wrote " << R << "x" << C << " decomposition to " << dumpFile << std::endl;
     }
+    if (device == "cpu") return run_cpu(*params, *obstacles, outDir, runs);
     const int ndev = lbm_device_count();
     if (ndev <= 0) {
         std::cerr << "No HIP device visible" << std::endl;
