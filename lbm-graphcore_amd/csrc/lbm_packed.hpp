@@ -35,20 +35,9 @@ __device__ __forceinline__ float dpp_from_left(float v) {  // lane - 1
 __device__ __forceinline__ float dpp_from_right(float v) {  // lane + 1
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
 }
-// (x-1) and (x+1) neighbours of a lane's column pair (A = .x, B = .y).  The
-// shifted half is written over its own source register and the pair is
-// viewed swapped: left2(v) = {dpp(v.y), v.x} lives in v's registers as
-// {v.x, dpp(v.y)}, and the compiler folds the swap into the op_sel of the
-// packed instructions that read it -- one v_mov_dpp per shifted pair instead
-// of a v_mov_dpp plus a v_mov_b32 for the unshifted half (a register pair
-// must be even-aligned, so {dpp(v.y), v.x} cannot be formed in place).
-// left2_sw / right2_sw return the register image itself (swapped halves),
-// for stores that keep the swap (the LP slots, lbm_stream2.hip).
-__device__ __forceinline__ f2 left2_sw(f2 v) { return f2{v.x, dpp_from_left(v.y)}; }
-__device__ __forceinline__ f2 right2_sw(f2 v) { return f2{dpp_from_right(v.x), v.y}; }
-__device__ __forceinline__ f2 swap2(f2 v) { return __builtin_shufflevector(v, v, 1, 0); }
-__device__ __forceinline__ f2 left2(f2 v) { return swap2(left2_sw(v)); }
-__device__ __forceinline__ f2 right2(f2 v) { return swap2(right2_sw(v)); }
+// (x-1) and (x+1) neighbours of a lane's column pair (A = .x, B = .y)
+__device__ __forceinline__ f2 left2(f2 v) { return f2{dpp_from_left(v.y), v.x}; }
+__device__ __forceinline__ f2 right2(f2 v) { return f2{v.y, dpp_from_right(v.x)}; }
 
 // RN(x / d) for d = 9 or 36 (see header)
 template <int D>

@@ -240,21 +240,14 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
             // ~5 v_mov_b64 per level and row): planes 2, 5, 6 of row y from the
             // LDS slot into the registers, row y+1 into the slot (read before
             // write: one wave's LDS operations stay in order), planes 0, 1, 3
-            // of row y+1.  Planes 5 and 6 sit in their slots with swapped
-            // halves (left2_sw / right2_sw: the shifted pair as it lies in the
-            // registers) and are read back as two dwords, so neither side
-            // spends a move on the swap
+            // of row y+1
             f2 *slot = lpl + b * 3 * 64;
             st.p2[0][b] = slot[0];
-            {
-                const float *q5 = reinterpret_cast<const float *>(&slot[64]);
-                const float *q6 = reinterpret_cast<const float *>(&slot[128]);
-                st.p5[0][b] = f2{q5[1], q5[0]};
-                st.p6[0][b] = f2{q6[1], q6[0]};
-            }
+            st.p5[0][b] = slot[64];
+            st.p6[0][b] = slot[128];
             slot[0] = cur[2];
-            slot[64] = left2_sw(cur[5]);
-            slot[128] = right2_sw(cur[6]);
+            slot[64] = left2(cur[5]);
+            slot[128] = right2(cur[6]);
             st.c0[b] = cur[0];
             st.c1[b] = left2(cur[1]);
             st.c3[b] = right2(cur[3]);
@@ -263,11 +256,9 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         if (rowlive) {
             const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
             const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
-            if constexpr (LP)  // LP: the per-level |u| sums in LDS, not VGPRs -- an LDS add with no
-                // return (ds_add_f32): a read-modify-write would make the wave wait for its
-                // LDS reads (this level's slot reads included) at every level.  One lane,
-                // one address: the adds land in program order, as the RMW's did
-                __hip_atomic_fetch_add(&lps[b * 64], ua + ub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if constexpr (LP)
+                lps[b * 64] += ua + ub;  // LP: the per-level |u| sums in LDS, not VGPRs (as an LDS
+                                         // float atomic add with no return: 1.6x slower, profiles/r04/ab_libs.log)
             else
                 st.tot[b] += ua + ub;
         }
