@@ -1005,6 +1005,9 @@ struct lbm_handle {
         // (smallest tile height with one tile per CU first, except that 2-row
         // tiles are slower than 4-row ones on every grid measured:
         // profiles/r01/resident/)
+        // v5 (two-cell ring, one hand-off per two steps): whole 128 x 32 tiles only
+        if (res_version == 5 && p.nx % RES_TWV[RES5_32] == 0 && p.ny % RES_TH[RES5_32] == 0)
+            order.push_back(RES5_32);
         if (p.nx % 2 == 0 && (res_version == 0 || res_version == 2))
             order.insert(order.end(), {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2, RES2_16x8});
         if (res_version == 0 || res_version == 1) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});
@@ -1014,7 +1017,7 @@ struct lbm_handle {
             const int tx = (p.nx + RES_TWV[v] - 1) / RES_TWV[v];
             const int ty = (p.ny + RES_TH[v] - 1) / RES_TH[v];
             int cap = 0;
-            HIP_CHECK(resident_capacity(v, s.dev, tolerance && RES_VER[v] == 2, cap));
+            HIP_CHECK(resident_capacity(v, s.dev, tolerance && RES_VER[v] >= 2, cap));
             const long long n = (long long)tx * ty;
             if (n <= cap && n <= (long long)res_per_cu * cus) {
                 res_variant = v;
@@ -1024,7 +1027,7 @@ struct lbm_handle {
             }
         }
         if (res_variant < 0) return false;
-        const size_t granules = 2ull * res_tx * res_ty * 8 * 3 * RES_GW;
+        const size_t granules = 2ull * res_tx * res_ty * 8 * RES_GV[res_variant] * RES_GW;
         // granules validate by their step tag (== the expected step, never 0 or
         // all-ones in a run): the poison pattern reads as "not there yet"
         HIP_CHECK(hipMalloc(&res_halo, granules * sizeof(unsigned long long)));
@@ -1099,7 +1102,7 @@ struct lbm_handle {
                 HIP_CHECK(hipMemsetAsync(htrace, 0, n, s.s_comp));
                 a.htrace = htrace;
             }
-            HIP_CHECK(launch_resident(a, res_variant, tolerance && RES_VER[res_variant] == 2, s.s_comp));
+            HIP_CHECK(launch_resident(a, res_variant, tolerance && RES_VER[res_variant] >= 2, s.s_comp));
             if (htrace) {  // per tile and step: wait for the slowest neighbour, then the hop itself
                 std::vector<unsigned long long> hv((size_t)2 * trace_steps * ntiles);
                 HIP_CHECK(hipMemcpyAsync(hv.data(), htrace, hv.size() * 8, hipMemcpyDeviceToHost, s.s_comp));
@@ -2131,7 +2134,7 @@ int lbm_placement_probe(lbm_handle *h, int32_t *kept, int32_t *tried, float *ms_
 int32_t lbm_numerics(lbm_handle *h) {
     if (!h) return -1;
     if (!h->tolerance || h->pipeline) return 0;
-    if (h->resident) return RES_VER[h->res_variant] == 2 ? 1 : 0;
+    if (h->resident) return RES_VER[h->res_variant] >= 2 ? 1 : 0;
     return (h->use_stream && h->fused) ? 1 : 0;
 }
 

@@ -189,12 +189,16 @@ constexpr int RES2_TW = 128;
 enum ResVariant : int {
     RES_64 = 0, RES_32 = 1, RES_16 = 2, RES_16x4 = 3, RES_8 = 4, RES_4 = 5,           // v1
     RES2_32 = 6, RES2_16 = 7, RES2_8 = 8, RES2_4 = 9, RES2_2 = 10,                    // v2
-    RES2_16x8 = 11                                                                      // v2, 8 waves: 2 tiles per CU
+    RES2_16x8 = 11,                                                                     // v2, 8 waves: 2 tiles per CU
+    RES5_32 = 12                                                                        // v5: two-cell ring (lbm_resident2.hip)
 };
-constexpr int NUM_RES = 12;
-constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 16};
-constexpr int RES_TWV[NUM_RES] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128, 128};
-constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2};
+constexpr int NUM_RES = 13;
+constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 16, 32};
+constexpr int RES_TWV[NUM_RES] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128, 128, 128};
+constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 5};
+// granule values per (tile, direction, position): v1/v2 three planes; v5 the
+// nine values of a two-deep band (lbm_resident2.hip)
+constexpr int RES_GV[NUM_RES] = {3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 9};
 constexpr int RES_GW = 128;  // granule positions per (tile, direction, plane), both versions
 
 struct ResidentArgs {

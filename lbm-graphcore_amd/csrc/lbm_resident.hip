@@ -607,6 +607,8 @@ __global__ __launch_bounds__(256) void resident_reduce(const float *partials, fl
 
 // ---- host side ---------------------------------------------------------------
 
+const void *resident_kernel_r2(bool tol, int &threads);  // lbm_resident2.hip
+
 namespace {
 template <int NW, int R>
 const void *resident_fn() {
@@ -624,6 +626,7 @@ const void *resident_fn2(bool tol) {
 // scalar v1 tiles have only the bitwise one
 const void *resident_kernel(int variant, int &threads, bool tol) {
     switch (variant) {
+        case RES5_32: return resident_kernel_r2(tol, threads);  // lbm_resident2.hip
         case RES_64: threads = 1024; return resident_fn<16, 4>();
         case RES_32: threads = 1024; return resident_fn<16, 2>();
         case RES_16: threads = 1024; return resident_fn<16, 1>();

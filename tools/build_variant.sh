@@ -1,16 +1,17 @@
 #!/bin/bash
-# Build a variant of liblbm_hip.so with extra compile definitions for the
-# stream kernel (lbm_stream2.hip) only, linked with the default objects:
-#   tools/build_variant.sh NAME "-DLBM_EXP_X=1 ..."  ->  build_var/NAME/liblbm_hip.so
+# Build a variant of liblbm_hip.so with extra compile definitions for ONE
+# source file (default lbm_stream2.hip), linked with the default objects:
+#   tools/build_variant.sh NAME "-DLBM_EXP_X=1 ..." [SOURCE]  ->  build_var/NAME/liblbm_hip.so
 # (select it at run time with LBM_HIP_LIB=build_var/NAME/liblbm_hip.so)
 set -e
 HERE=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$HERE/lbm-graphcore_amd
 OUT=$HERE/build_var/$1
+SRC=${3:-lbm_stream2}
 mkdir -p "$OUT"
 make -s -C "$PKG" lib
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -I"$HERE/include" -I"$PKG/csrc" $2 \
-  -c -o "$OUT/lbm_stream2.o" "$PKG/csrc/lbm_stream2.hip"
-OBJS=$(ls "$PKG"/build/obj/*.o | grep -v lbm_stream2.o)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/liblbm_hip.so" $OBJS "$OUT/lbm_stream2.o" -lrccl
+  -c -o "$OUT/$SRC.o" "$PKG/csrc/$SRC.hip"
+OBJS=$(ls "$PKG"/build/obj/*.o | grep -v "/$SRC.o")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/liblbm_hip.so" $OBJS "$OUT/$SRC.o" -lrccl
 echo "built $OUT/liblbm_hip.so"
