@@ -343,13 +343,13 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         secs, dev = float(t[0]), float(t[1])
     cells = n ** 3
-    # two steps per pass (step3d_two: 60 x 8 owned of 64 x 12 loaded cells per
-    # plane -> (19 x 4 B x (768/480 + 1)) / 2 = 98.8 B per update) on one slab and
-    # on z slabs of >= 4 planes; 152 B per update for the one-step kernel; in
-    # tolerance mode (one slab, or z slabs of >= 6 planes): three steps per pass (step3d_three: 58 x 6 owned
-    # -> (19 x 4 B x (768/348 + 1)) / 3 = 81.2 B), the rest in two-step passes
+    # three steps per pass on one slab or z slabs of >= 6 planes, both numerics
+    # (step3d_three: 58 x 6 owned of 64 x 12 loaded cells per plane ->
+    # (19 x 4 B x (768/348 + 1)) / 3 = 81.2 B per update), the rest in two-step
+    # passes (step3d_two: 60 x 8 owned -> (19 x 4 B x (768/480 + 1)) / 2 =
+    # 98.8 B) on z slabs of >= 4 planes; 152 B per update for the one-step kernel
     two = nzs >= 4
-    three = two and bool(flags & native.FLAG_TOLERANCE) and (nzs >= 6 or not dist_on)
+    three = two and (nzs >= 6 or not dist_on)
     b2, b3 = 19 * 4 * (768 / 480 + 1) / 2, 19 * 4 * (768 / 348 + 1) / 3
     n3 = steps // 3 * 3 if three else 0
     n2 = (steps - n3) // 2 * 2 if two else 0

@@ -35,8 +35,9 @@
  * planes below and above; the domain is cut into z slabs (one per rank /
  * sub-domain); one-step launches move each slab's top plane speeds 9..13 and
  * bottom plane speeds 14..18 to the neighbour's ghost planes, two-step passes
- * two whole planes each way, and a single slab in tolerance mode runs three
- * steps per pass (its ghost planes refreshed from the periodic images).
+ * two whole planes each way, three-step passes (the default for one slab or
+ * slabs of >= 6 planes, both numerics) three planes each way (a single slab's
+ * ghost planes refreshed from the periodic images).
  *
  * Placement reuses lbm_config (lbm_hip.h): parts = z slabs, transport LOCAL
  * (all slabs in this process, device copies) or RCCL (one slab per rank);
@@ -69,11 +70,11 @@ typedef struct lbm3d_params {
 typedef struct lbm3d_handle lbm3d_handle;
 
 /* Create the engine: obstacles uint8[nz][ny][nx] (full domain).
- * Bitwise-mode single-slab engines of >= 2^26 cells run a placement probe
- * here: up to four candidate lattice pairs, at most
- * 96 GB of device memory held transiently (about 82 GB at 512^3), the fastest
- * kept and the rest freed before the call returns.  Tolerance-mode engines
- * (three-step passes) skip it. */
+ * Single-slab engines of >= 2^26 cells that run two-step passes (three-step
+ * passes off: LBM3D_THREE=0) run a placement probe here (DESIGN.md section
+ * 4.9): up to four candidate lattice pairs, at most 96 GB of device memory
+ * held transiently (about 82 GB at 512^3), the fastest kept and the rest freed
+ * before the call returns.  Engines on three-step passes (the default) skip it. */
 int lbm3d_create(const lbm3d_params *params, const uint8_t *obstacles, const lbm_config *config,
                  lbm3d_handle **out);
 

@@ -623,7 +623,9 @@ constexpr int T3TH3 = 12;       // rows (waves) per block
 constexpr int T3OY3 = T3TH3 - 6;
 constexpr int GZ3 = 3;  // ghost planes each side of every slab lattice (and obst_g)
 
-template <bool TOL>
+// SKIP: rows no later level reads skip the collision (level 1: rows 1..10,
+// level 2: 2..9, level 3: 3..8 live), as step3d_two's SKIP.
+template <bool TOL, bool SKIP>
 __global__ __launch_bounds__(T3W *T3TH3) void step3d_three(Two3Args a) {
     __shared__ float lds1[T3<T3TH3>::LDS], lds2[T3<T3TH3>::LDS], lds3[T3<T3TH3>::LDS];
     __shared__ float red[3][T3TH3];
@@ -658,15 +660,19 @@ __global__ __launch_bounds__(T3W *T3TH3) void step3d_three(Two3Args a) {
         ob2 = ob1;
         ob1 = obz(j - 1);
         float o1[Q3], o2[Q3], o3[Q3];
-        const float v1 = level3<T3TH3, TOL>(in, o1, lds1, j, r0a, r9aa, r9ba, zra, lane, wy, ob1, true, a);
+        constexpr int R = T3TH3;
+        const float v1 = level3<T3TH3, TOL>(in, o1, lds1, j, r0a, r9aa, r9ba, zra, lane, wy, ob1,
+                                            !SKIP || (wy >= 1 && wy < R - 1), a);
         if (own && j - 1 >= zs && j - 1 < ze) u1 += v1;
         // level 1 is done with plane j: its registers take plane j + 1, in
         // flight across levels 2 and 3
 #pragma unroll
         for (int k = 0; k < Q3; ++k) in[k] = pn[k * a.KS];
-        const float v2 = level3<T3TH3, TOL>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, zrb, lane, wy, ob2, true, a);
+        const float v2 = level3<T3TH3, TOL>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, zrb, lane, wy, ob2,
+                                            !SKIP || (wy >= 2 && wy < R - 2), a);
         if (own && j - 2 >= zs && j - 2 < ze) u2 += v2;
-        const float v3 = level3<T3TH3, TOL>(o2, o3, lds3, j - 2, r0c, r9ac, r9bc, zrc, lane, wy, ob3, true, a);
+        const float v3 = level3<T3TH3, TOL>(o2, o3, lds3, j - 2, r0c, r9ac, r9bc, zrc, lane, wy, ob3,
+                                            !SKIP || (wy >= 3 && wy < R - 3), a);
         if (own && j - 3 >= zs && j - 3 < ze) {
             u3 += v3;
             float *d = a.fout + (long long)(j - 3) * a.PL + row;
@@ -803,15 +809,21 @@ struct lbm3d_handle {
     bool two = true;   // LBM3D_TWO: two steps per pass (step3d_two), single slab or z slabs
     // LBM3D_THREE: three steps per pass (step3d_three), one slab or z slabs of
     // >= 6 planes (needs two);
-    // default (-1): in tolerance mode only -- 512^3: tolerance 50.2-50.6 vs
-    // 43.5-43.9 GLUPS for two-step passes, bitwise 43.9-44.1 vs 44.6-45.0 (the
-    // bitwise collision's divisions make the third level's recompute VALU-bound;
-    // profiles/r03/d3q19/ab_three.log)
+    // default (-1): both modes since round 4 (with skip3) -- 512^3, skip3 on:
+    // tolerance 55.4-55.6 GLUPS, bitwise 51.2-51.3 vs 44.1-45.2 for two-step
+    // passes (profiles/r04/d3q19/ab_skip3.log); round 3, skip3 off, had kept
+    // bitwise on two-step passes (43.9-44.1 vs 44.6-45.0: the divisions made
+    // the third level's recompute VALU-bound)
     int three = -1;
     int seg3 = 64;     // LBM3D_SEG3: z planes per block of the three-step kernel
     int seg = 64;      // LBM3D_SEG: z planes per block of the two-step kernel (32-128 equal within noise at 512^3)
     int th = 12;       // LBM3D_TH: rows (waves) per block of the two-step kernel (12 only since round 3)
     bool skip = false; // LBM3D_SKIP: waves skip the collisions of rows no later level reads (not faster)
+    // LBM3D_SKIP3: the same in the three-step pass -- there it pays (default on):
+    // the live rows per level (10, 8, 6 of 12) spread over the 4 SIMDs as
+    // 3 + 2 + 2 wave-collisions on the busiest SIMD instead of 3 + 3 + 3;
+    // 512^3 tolerance 55.4-55.6 vs 45.6-50.0 GLUPS, bitwise 51.2-51.3 vs 43.7-43.9
+    bool skip3 = true;
     // LBM3D_PD: input planes in flight in the two-step kernel -- 0 (default): the
     // next plane loaded once level 1 has consumed the current one (44.7 vs
     // 38.6-42.5 GLUPS at 512^3 for 1, profiles/r03/d3q19/ab_pd.log); 1, 2
@@ -875,6 +887,7 @@ struct lbm3d_handle {
         if (const char *g = knob("LBM3D_SEG3")) seg3 = std::max(1, atoi(g));
         if (const char *h = knob("LBM3D_TH")) th = atoi(h);
         if (const char *k = knob("LBM3D_SKIP")) skip = atoi(k) != 0;
+        if (const char *k = knob("LBM3D_SKIP3")) skip3 = atoi(k) != 0;
         if (const char *d = knob("LBM3D_PD")) pd = atoi(d);
         if (const char *k = knob("LBM3D_KSPAD")) kspad = (std::max(0LL, atoll(k)) + 63) / 64 * 64;
         lattice_pad = knob("LBM_LATTICE_PAD");
@@ -963,10 +976,10 @@ struct lbm3d_handle {
     // pair is filled as a fresh allocation is, so the engine's state is as if
     // the probe had not run.  Failures inside free every extra candidate and
     // restore the original pair.
-    // Scope: bitwise-mode engines (two-step passes).  Tolerance-mode runs use
-    // three-step passes, whose spread over lattice placements has not been
-    // measured to follow the two-step pass's, so they skip the probe (and its
-    // transient ~82 GB of candidate pairs at 512^3).
+    // Scope: engines on two-step passes.  Three-step engines (the default in
+    // both numerics since round 4) skip it: timing two-step passes for them
+    // gained nothing measurable (profiles/r04/prof1/d3_probe.log), and the
+    // probe holds ~82 GB of candidate pairs transiently at 512^3.
     void placement_probe() {
         if (multi() || !use_two() || (use_three() && !probe_tol) || slabs.size() != 1) return;
         Slab &s = slabs[0];
@@ -1194,7 +1207,7 @@ struct lbm3d_handle {
     // three-step passes: one slab, or z slabs of at least 6 planes (ghosts are
     // 3 planes of the neighbours, exchanged once per pass)
     bool use_three() const {
-        if (!(three < 0 ? tolerance : three != 0) || !use_two()) return false;
+        if (three == 0 || !use_two()) return false;
         if (!multi()) return true;
         for (int n : all_nz)
             if (n < 6) return false;
@@ -1238,10 +1251,14 @@ struct lbm3d_handle {
         a.blk0 = blk0;
         const dim3 g((p.nx + T3OX3 - 1) / T3OX3, (p.ny + T3OY3 - 1) / T3OY3, (zn - z0 + seg3 - 1) / seg3);
         const dim3 b(T3W, T3TH3);
-        if (tolerance)
-            hipLaunchKernelGGL((step3d_three<true>), g, b, 0, st, a);
+        if (tolerance && skip3)
+            hipLaunchKernelGGL((step3d_three<true, true>), g, b, 0, st, a);
+        else if (tolerance)
+            hipLaunchKernelGGL((step3d_three<true, false>), g, b, 0, st, a);
+        else if (skip3)
+            hipLaunchKernelGGL((step3d_three<false, true>), g, b, 0, st, a);
         else
-            hipLaunchKernelGGL((step3d_three<false>), g, b, 0, st, a);
+            hipLaunchKernelGGL((step3d_three<false, false>), g, b, 0, st, a);
         H3(hipGetLastError());
     }
 

@@ -268,14 +268,16 @@ def test_d3q19_two_step_block_rows_bitwise(gpu_lib, nx, ny, nz, parts, th, skip,
 @pytest.mark.parametrize("seg3", ["64", "5", "1"])
 @pytest.mark.parametrize("nx,ny,nz", [(13, 9, 7), (64, 8, 5), (1, 5, 3), (130, 3, 2), (61, 17, 1), (125, 23, 9),
                                       (58, 6, 4), (59, 13, 12), (2, 6, 3)])
-def test_d3q19_three_step_bitwise(gpu_lib, nx, ny, nz, seg3, monkeypatch):
+@pytest.mark.parametrize("skip3", ["1", "0"])
+def test_d3q19_three_step_bitwise(gpu_lib, nx, ny, nz, seg3, skip3, monkeypatch):
     """Three steps per pass (step3d_three, single slab, the default there):
     10 steps = three passes + one one-step launch, 8 = two passes + one
     two-step pass; owned tiles of 58 x 6 (partial and wrapped in x and y:
     nx, ny below and above one tile), z segments of 64, 5 and 1 planes, slabs
-    thinner than the three ghost planes (nz < 3).  Bitwise vs the oracle
-    (LBM3D_THREE=1: by default the three-step pass runs in tolerance mode only)."""
+    thinner than the three ghost planes (nz < 3).  Bitwise vs the oracle, with
+    the dead-row skip (LBM3D_SKIP3, the default) and without it."""
     monkeypatch.setenv("LBM3D_THREE", "1")
+    monkeypatch.setenv("LBM3D_SKIP3", skip3)
     monkeypatch.setenv("LBM3D_SEG3", seg3)
     p, obst, c0 = _problem(nx, ny, nz, 3 * nx + ny + nz)
     for steps in (10, 8):
@@ -390,6 +392,7 @@ def test_d3q19_placement_probe_transparent(gpu_lib, flags, monkeypatch):
     three candidate pairs) leaves the engine as a fresh one: bitwise the same
     lattice and av_vels as with the probe off, and (bitwise mode) as the oracle."""
     p, obst, c0 = _problem(70, 31, 24, 5)
+    monkeypatch.setenv("LBM3D_THREE", "0")  # the probe serves two-step engines (three-step ones skip it)
     out = []
     for tries in ("1", "3"):
         monkeypatch.setenv("LBM3D_PLACEMENT_TRIES", tries)

@@ -121,9 +121,9 @@ def test_d3q19_512_eight_slabs_bitwise(gpu_lib):
         with gpu_lib.Engine3D(p, obst, parts=parts, devices=[0]) as e:
             assert len(e.local_slabs()) == parts
             e.init_equilibrium()
-            e.run_steps(3)           # odd: two-step pass(es) + a one-step launch on one slab
+            e.run_steps(3)           # one three-step pass (slabs of 64 planes: three-plane exchange)
             c3, av3 = e.store(n_av=3)
-            e.run_steps(4)
+            e.run_steps(4)           # a three-step pass + a one-step launch
             c7, av7 = e.store(n_av=4)
         outs[parts] = (c3, av3, c7, av7)
     one, eight = outs[1], outs[8]
