@@ -1345,10 +1345,15 @@ struct lbm_handle {
             HIP_CHECK(hipEventRecord(s.ev_u, s.s_comm));
             return;
         }
-        // LOCAL: receiver pulls each message with a device (peer) copy
+        // LOCAL: receiver pulls each message with a device (peer) copy.  The
+        // unpack into s's own lattice also waits for s's own pack / boundary
+        // event: without it, when the neighbours ran ahead, the pipeline's
+        // unpack of step t rewrote s's ghost ring while s's propagate of step
+        // t-1 was still reading it (intermittent, test_pipeline_decomposed_bitwise)
         for (size_t k = 0; k < subs.size(); ++k) {
             Sub &s = subs[k];
             set_device(s);
+            HIP_CHECK(hipStreamWaitEvent(s.s_comm, s.ev_b, 0));
             for (int e = 0; e < 8; ++e) {
                 if (!s.remote[e]) continue;
                 Sub *src = local_sub(s.nb[e]);
