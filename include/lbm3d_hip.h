@@ -70,11 +70,10 @@ typedef struct lbm3d_params {
 typedef struct lbm3d_handle lbm3d_handle;
 
 /* Create the engine: obstacles uint8[nz][ny][nx] (full domain).
- * Single-slab engines of >= 2^26 cells that run two-step passes (three-step
- * passes off: LBM3D_THREE=0) run a placement probe here (DESIGN.md section
- * 4.9): up to four candidate lattice pairs, at most 96 GB of device memory
- * held transiently (about 82 GB at 512^3), the fastest kept and the rest freed
- * before the call returns.  Engines on three-step passes (the default) skip it. */
+ * Single-slab engines of >= 2^26 cells run a placement probe here (DESIGN.md
+ * section 4.9): up to six candidate lattice pairs timed with the engine's own
+ * pass form, at most 128 GB of device memory held transiently (about 124 GB
+ * at 512^3), the fastest kept and the rest freed before the call returns. */
 int lbm3d_create(const lbm3d_params *params, const uint8_t *obstacles, const lbm_config *config,
                  lbm3d_handle **out);
 

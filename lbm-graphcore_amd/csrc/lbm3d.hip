@@ -831,9 +831,9 @@ struct lbm3d_handle {
     long long kspad = 0;  // LBM3D_KSPAD: floats appended to each speed plane (multiple of 64)
     const char *lattice_pad = nullptr;  // LBM_LATTICE_PAD (debug knob)
     bool poison = false;  // LBM_POISON=1: fresh allocations filled with NaN bytes
-    int probe_tries = 4;  // LBM3D_PLACEMENT_TRIES: lattice pairs the placement probe times (1 = off)
+    int probe_tries = 6;  // LBM3D_PLACEMENT_TRIES: lattice pairs the placement probe times (1 = off)
     long long probe_min_cells = 1LL << 26;  // LBM3D_PROBE_MIN_CELLS: smallest single slab probed
-    bool probe_tol = false;                  // LBM3D_PROBE_TOL=1: probe tolerance-mode engines too (A/B)
+    bool probe_three = true;                 // LBM3D_PROBE_THREE=0: three-step engines skip the probe (A/B)
     bool probe_log = false;  // LBM_PLACEMENT_LOG: print the probe's per-pair times
     bool tolerance = false;  // LBM_FLAG_TOLERANCE: the two-step passes use cell3dt (not bitwise)
     std::vector<Slab> slabs;
@@ -893,7 +893,7 @@ struct lbm3d_handle {
         lattice_pad = knob("LBM_LATTICE_PAD");
         if (const char *t = knob("LBM3D_PLACEMENT_TRIES")) probe_tries = std::max(1, atoi(t));
         if (const char *m = knob("LBM3D_PROBE_MIN_CELLS")) probe_min_cells = std::max(0LL, atoll(m));
-        if (const char *pt = knob("LBM3D_PROBE_TOL")) probe_tol = atoi(pt) != 0;
+        if (const char *pt = knob("LBM3D_PROBE_THREE")) probe_three = atoi(pt) != 0;
         probe_log = knob("LBM_PLACEMENT_LOG") != nullptr;
         if (tolerance) {  // the tolerance pass exists for the default block only
             th = 12;
@@ -970,23 +970,27 @@ struct lbm3d_handle {
     // +-5 % at 512^3 fixed by where the lattices land (39.9-44.2 GLUPS over
     // six engines in one process, profiles/r03/d3q19/spread.log).  A single
     // slab of at least 2^26 cells allocates up to probe_tries lattice pairs
-    // (at most 96 GB held at once: four at 512^3), times two-step passes on
-    // each (constant populations; one warm-up round, then the best of two
+    // (at most 128 GB held at once: six at 512^3), times the engine's passes
+    // on each (constant populations; one warm-up round, then the best of two
     // interleaved rounds), keeps the fastest pair and frees the rest; the kept
     // pair is filled as a fresh allocation is, so the engine's state is as if
     // the probe had not run.  Failures inside free every extra candidate and
     // restore the original pair.
-    // Scope: engines on two-step passes.  Three-step engines (the default in
-    // both numerics since round 4) skip it: timing two-step passes for them
-    // gained nothing measurable (profiles/r04/prof1/d3_probe.log), and the
-    // probe holds ~82 GB of candidate pairs transiently at 512^3.
+    // Scope: single-slab engines; each candidate is timed with the engine's
+    // own pass form (three-step passes, the default in both numerics since
+    // round 4, or two-step ones).  Round 4 first timed two-step passes for
+    // three-step engines and gained nothing (profiles/r04/prof1/d3_probe.log);
+    // timing their own three-step passes it keeps the fast placement
+    // (7.1-7.2 vs 7.4-7.8 ms per tolerance pass): 55.0-55.9 GLUPS over four
+    // engines against 51.5-55.4 unprobed (profiles/r04/d3q19/ab_probe3.log).
+    // LBM3D_PROBE_THREE=0 skips the probe for three-step engines (A/B).
     void placement_probe() {
-        if (multi() || !use_two() || (use_three() && !probe_tol) || slabs.size() != 1) return;
+        if (multi() || !use_two() || (use_three() && !probe_three) || slabs.size() != 1) return;
         Slab &s = slabs[0];
         if ((long long)p.nx * p.ny * p.nz < probe_min_cells || s.f_joint) return;
         const size_t floats = (size_t)(s.nzs + 2 * GZ3) * PL;
         const size_t pair_bytes = 2 * sizeof(float) * floats;
-        const int cap = (int)std::max<size_t>(1, (96ull << 30) / pair_bytes);
+        const int cap = (int)std::max<size_t>(1, (128ull << 30) / pair_bytes);
         const int tries = std::min({probe_tries, 8, cap});
         if (tries <= 1) return;
         H3(hipSetDevice(s.dev));
@@ -1000,6 +1004,7 @@ struct lbm3d_handle {
             s.cur = 0;
         };
         hipEvent_t e0 = nullptr, e1 = nullptr;
+        const bool three_probe = use_three();
         try {
             for (int c = 1; c < tries; ++c) {
                 std::array<float *, 2> f{nullptr, nullptr};
@@ -1020,8 +1025,11 @@ struct lbm3d_handle {
                 for (size_t c = 0; c < cand.size(); ++c) {
                     set_pair(c);
                     H3(hipEventRecord(e0, s.s_comp));
-                    for (int i = 0; i < 2; ++i) {
-                        launch_two(s, 0, s.nzs, 0, s.s_comp);
+                    for (int i = 0; i < 2; ++i) {  // the engine's own pass form
+                        if (three_probe)
+                            launch_three(s, 0, s.nzs, 0, s.s_comp);
+                        else
+                            launch_two(s, 0, s.nzs, 0, s.s_comp);
                         s.cur ^= 1;
                     }
                     H3(hipEventRecord(e1, s.s_comp));
@@ -1033,7 +1041,8 @@ struct lbm3d_handle {
             for (size_t c = 1; c < cand.size(); ++c)
                 if (best[c] < best[keep]) keep = c;
             if (probe_log) {
-                fprintf(stderr, "lbm3d placement probe (%dx%dx%d): ms per two-step pass", p.nx, p.ny, p.nz);
+                fprintf(stderr, "lbm3d placement probe (%dx%dx%d): ms per %s-step pass", p.nx, p.ny, p.nz,
+                        three_probe ? "three" : "two");
                 for (float v : best) fprintf(stderr, " %.4f", v);
                 fprintf(stderr, "; kept pair %zu\n", keep);
             }

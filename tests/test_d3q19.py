@@ -387,12 +387,13 @@ def test_d3q19_tolerance_vs_oracle(gpu_lib, parts):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("flags", [0, 4])
-def test_d3q19_placement_probe_transparent(gpu_lib, flags, monkeypatch):
+@pytest.mark.parametrize("three", ["1", "0"])
+def test_d3q19_placement_probe_transparent(gpu_lib, flags, three, monkeypatch):
     """The D3Q19 placement probe (forced on a small slab: LBM3D_PROBE_MIN_CELLS=0,
     three candidate pairs) leaves the engine as a fresh one: bitwise the same
     lattice and av_vels as with the probe off, and (bitwise mode) as the oracle."""
     p, obst, c0 = _problem(70, 31, 24, 5)
-    monkeypatch.setenv("LBM3D_THREE", "0")  # the probe serves two-step engines (three-step ones skip it)
+    monkeypatch.setenv("LBM3D_THREE", three)  # the probe times the engine's own pass form
     out = []
     for tries in ("1", "3"):
         monkeypatch.setenv("LBM3D_PLACEMENT_TRIES", tries)
