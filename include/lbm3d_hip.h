@@ -99,6 +99,19 @@ int64_t lbm3d_total_free_cells(lbm3d_handle *h);
 /* Local slab z ranges: z0[i], nz[i] for i < *n_out (LOCAL: all; RCCL: this rank's). */
 int lbm3d_local_slabs(lbm3d_handle *h, int32_t *z0, int32_t *nz, int32_t max_slabs, int32_t *n_out);
 
+/*
+ * The ordered ghost-exchange posts of z slab `rank` of `parts` (host-only;
+ * the engine's RCCL exchanges iterate the same list, lbm3d.hip slab_posts):
+ * send up (dir 0, +z), send down (dir 1), receive the below ghosts (dir 1),
+ * receive the above ghosts (dir 0), periodic in z.  planes = 1: the five
+ * speed planes leaving a face (one-step launches); 2 / 3: that many whole
+ * planes, all 19 speeds (two- / three-step passes).  floats use the engine's
+ * default plane layout (rows padded to 16 floats).  Writes 4 lbm_xfer
+ * (lbm_hip.h) to out (may be NULL) and *n_out = 4.
+ */
+int lbm3d_exchange_schedule(int32_t nx, int32_t ny, int32_t nz, int32_t parts, int32_t rank, int32_t planes,
+                            lbm_xfer *out, int32_t max_out, int32_t *n_out);
+
 const char *lbm3d_last_error(lbm3d_handle *h);
 
 void lbm3d_destroy(lbm3d_handle *h);

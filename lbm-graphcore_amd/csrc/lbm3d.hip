@@ -752,11 +752,25 @@ __global__ __launch_bounds__(BLOCK) void soa_to_aos3d(const float *f, float *aos
     for (int k = 0; k < Q3; ++k) aos[i * Q3 + k] = s[k * KS];
 }
 
+hipError_t launch_debug_spin(int microseconds, hipStream_t s);  // lbm_kernels.hip
 }  // namespace lbm
 
 using namespace lbm;
 
 namespace {
+
+// The ordered posts of one z slab's ghost exchange (RCCL pairs them by
+// order inside one ncclGroupStart/End): send up (dir 0, +z) to rank+1, send
+// down (dir 1, -z) to rank-1, receive the below ghosts (dir 1) from rank-1,
+// receive the above ghosts (dir 0) from rank+1 -- periodic in z.  `floats`
+// per message: 5 speed planes for a one-step launch, n whole planes (all 19
+// speeds) for an n-step pass.  exchange() / exchange_planes() post exactly
+// this list; lbm3d_exchange_schedule exports it.
+std::array<lbm_xfer, 4> slab_posts(int rank, int world, long long floats) {
+    const int up = (rank + 1) % world, down = (rank + world - 1) % world;
+    return {lbm_xfer{LBM_XFER_SEND, 0, up, 0, floats}, lbm_xfer{LBM_XFER_SEND, 1, down, 0, floats},
+            lbm_xfer{LBM_XFER_RECV, 1, down, 0, floats}, lbm_xfer{LBM_XFER_RECV, 0, up, 0, floats}};
+}
 
 struct fail3 : std::runtime_error {
     int code;
@@ -835,6 +849,10 @@ struct lbm3d_handle {
     long long probe_min_cells = 1LL << 26;  // LBM3D_PROBE_MIN_CELLS: smallest single slab probed
     bool probe_three = true;                 // LBM3D_PROBE_THREE=0: three-step engines skip the probe (A/B)
     bool probe_log = false;  // LBM_PLACEMENT_LOG: print the probe's per-pair times
+    // ordering regression knobs (debug only, tests/test_gpu_ordering.py): slab
+    // LBM_DEBUG_DELAY_SUB's boundary and interior launches are each preceded
+    // by a stall of LBM_DEBUG_DELAY_US on their stream
+    int delay_sub = -1, delay_us = 0;
     bool tolerance = false;  // LBM_FLAG_TOLERANCE: the two-step passes use cell3dt (not bitwise)
     std::vector<Slab> slabs;
     std::vector<int> all_z0, all_nz;
@@ -895,6 +913,8 @@ struct lbm3d_handle {
         if (const char *m = knob("LBM3D_PROBE_MIN_CELLS")) probe_min_cells = std::max(0LL, atoll(m));
         if (const char *pt = knob("LBM3D_PROBE_THREE")) probe_three = atoi(pt) != 0;
         probe_log = knob("LBM_PLACEMENT_LOG") != nullptr;
+        if (const char *d = knob("LBM_DEBUG_DELAY_SUB")) delay_sub = atoi(d);
+        if (const char *d = knob("LBM_DEBUG_DELAY_US")) delay_us = std::min(std::max(atoi(d), 0), 100000);
         if (tolerance) {  // the tolerance pass exists for the default block only
             th = 12;
             skip = false;
@@ -1288,6 +1308,7 @@ struct lbm3d_handle {
             H3(hipSetDevice(s.dev));
             H3(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
             wait_x(s, s.s_bnd);
+            stall(s, s.s_bnd);
             const auto r = three_ranges(s);
             int blk = 0;
             for (size_t i = 0; i < r.size() && i < 2; ++i) {
@@ -1300,6 +1321,7 @@ struct lbm3d_handle {
         for (auto &s : slabs) {
             H3(hipSetDevice(s.dev));
             const auto r = three_ranges(s);
+            stall(s, s.s_comp);
             if (r.size() > 2)
                 launch_three(s, r[2].first, r[2].second,
                              three_blocks(r[0].first, r[0].second) + three_blocks(r[1].first, r[1].second), s.s_comp);
@@ -1352,12 +1374,13 @@ struct lbm3d_handle {
             H3(hipSetDevice(s.dev));
             hipStream_t st = use_comm ? s.s_comm : s.s_comp;
             H3(hipStreamWaitEvent(st, s.ev_b, 0));
-            const int up = (rank + 1) % world, down = (rank + world - 1) % world;
             N3(ncclGroupStart());
-            N3(ncclSend(top(s), n2, ncclFloat, up, comm, st));
-            N3(ncclSend(bottom(s), n2, ncclFloat, down, comm, st));
-            N3(ncclRecv(ghost_lo(s), n2, ncclFloat, down, comm, st));
-            N3(ncclRecv(ghost_hi(s), n2, ncclFloat, up, comm, st));
+            for (const lbm_xfer &x : slab_posts(rank, world, (long long)n2)) {
+                if (x.op == LBM_XFER_SEND)
+                    N3(ncclSend(x.dir == 0 ? top(s) : bottom(s), (size_t)x.floats, ncclFloat, x.peer, comm, st));
+                else
+                    N3(ncclRecv(x.dir == 1 ? ghost_lo(s) : ghost_hi(s), (size_t)x.floats, ncclFloat, x.peer, comm, st));
+            }
             N3(ncclGroupEnd());
             H3(hipEventRecord(s.ev_x, st));
             return;
@@ -1391,6 +1414,7 @@ struct lbm3d_handle {
             H3(hipSetDevice(s.dev));
             H3(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
             wait_x(s, s.s_bnd);
+            stall(s, s.s_bnd);
             const auto r = two_ranges(s);
             int blk = 0;
             for (size_t i = 0; i < r.size() && i < 2; ++i) {
@@ -1403,6 +1427,7 @@ struct lbm3d_handle {
         for (auto &s : slabs) {
             H3(hipSetDevice(s.dev));
             const auto r = two_ranges(s);
+            stall(s, s.s_comp);
             if (r.size() > 2) launch_two(s, r[2].first, r[2].second, two_blocks(r[0].first, r[0].second) +
                                                                           two_blocks(r[1].first, r[1].second), s.s_comp);
             H3(hipStreamWaitEvent(s.s_comp, s.ev_b, 0));
@@ -1472,13 +1497,16 @@ struct lbm3d_handle {
             H3(hipSetDevice(s.dev));
             hipStream_t st = use_comm ? s.s_comm : s.s_comp;
             H3(hipStreamWaitEvent(st, s.ev_b, 0));
-            const int up = (rank + 1) % world, down = (rank + world - 1) % world;
             N3(ncclGroupStart());
             // same posting order on every rank: send up, send down, recv from below, recv from above
-            N3(ncclSend(up_src(s, l), 5 * (size_t)KS, ncclFloat, up, comm, st));
-            N3(ncclSend(down_src(s, l), 5 * (size_t)KS, ncclFloat, down, comm, st));
-            N3(ncclRecv(below_ghost(s, l), 5 * (size_t)KS, ncclFloat, down, comm, st));
-            N3(ncclRecv(above_ghost(s, l), 5 * (size_t)KS, ncclFloat, up, comm, st));
+            for (const lbm_xfer &x : slab_posts(rank, world, 5 * KS)) {
+                if (x.op == LBM_XFER_SEND)
+                    N3(ncclSend(x.dir == 0 ? up_src(s, l) : down_src(s, l), (size_t)x.floats, ncclFloat, x.peer, comm,
+                                st));
+                else
+                    N3(ncclRecv(x.dir == 1 ? below_ghost(s, l) : above_ghost(s, l), (size_t)x.floats, ncclFloat,
+                                x.peer, comm, st));
+            }
             N3(ncclGroupEnd());
             H3(hipEventRecord(s.ev_x, st));
             return;
@@ -1499,6 +1527,10 @@ struct lbm3d_handle {
                 H3(hipMemcpyPeerAsync(above_ghost(s, l), s.dev, down_src(*above, l), above->dev, bytes, st));
             H3(hipEventRecord(s.ev_x, st));
         }
+    }
+
+    void stall(const Slab &s, hipStream_t st) {
+        if (delay_us > 0 && s.id == delay_sub) H3(launch_debug_spin(delay_us, st));
     }
 
     // st waits for this slab's last exchange and (LOCAL) its neighbours' (they read our faces)
@@ -1557,6 +1589,7 @@ struct lbm3d_handle {
             H3(hipSetDevice(s.dev));
             H3(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
             wait_x(s, s.s_bnd);
+            stall(s, s.s_bnd);
             launch(s, 0, 1, s.partials, s.s_bnd);
             if (s.nzs >= 2) launch(s, s.nzs - 1, 1, s.partials + blocks_for(1), s.s_bnd);
             H3(hipEventRecord(s.ev_b, s.s_bnd));
@@ -1567,6 +1600,7 @@ struct lbm3d_handle {
         // interior reads the faces B(t-1) wrote, already ordered by ev_b)
         for (auto &s : slabs) {
             H3(hipSetDevice(s.dev));
+            stall(s, s.s_comp);
             launch(s, 1, s.nzs - 2, s.partials + s.nblk_bnd, s.s_comp);
             H3(hipStreamWaitEvent(s.s_comp, s.ev_b, 0));
             hipLaunchKernelGGL(reduce3d, dim3(1), dim3(BLOCK), 0, s.s_comp, s.partials, s.nblk_all, s.av_local, t);
@@ -1830,6 +1864,21 @@ int lbm3d_local_slabs(lbm3d_handle *h, int32_t *z0, int32_t *nz, int32_t max_sla
     for (int i = 0; i < n && i < max_slabs; ++i) {
         if (z0) z0[i] = h->slabs[i].z0;
         if (nz) nz[i] = h->slabs[i].nzs;
+    }
+    return LBM_OK;
+}
+
+int lbm3d_exchange_schedule(int32_t nx, int32_t ny, int32_t nz, int32_t parts, int32_t rank, int32_t planes,
+                            lbm_xfer *out, int32_t max_out, int32_t *n_out) {
+    if (!n_out || nx < 1 || ny < 1 || parts < 1 || parts > nz || rank < 0 || rank >= parts || planes < 1 ||
+        planes > 3)
+        return LBM_E_INVALID;
+    const long long KS = (long long)ny * ((nx + 15) / 16 * 16);  // the engine's speed stride (64-byte rows)
+    const auto v = slab_posts(rank, parts, planes == 1 ? 5 * KS : (long long)planes * Q3 * KS);
+    *n_out = (int32_t)v.size();
+    if (out) {
+        if (max_out < (int32_t)v.size()) return LBM_E_INVALID;
+        for (size_t i = 0; i < v.size(); ++i) out[i] = v[i];
     }
     return LBM_OK;
 }

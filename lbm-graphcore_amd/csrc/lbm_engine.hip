@@ -69,6 +69,7 @@ hipError_t launch_pipe_collision(const float *t, float *f, const uint8_t *obst, 
 hipError_t launch_pipe_av(const float *partials, int n, float *av_local, int t, hipStream_t s);
 hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, hipStream_t s);
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s);
+hipError_t launch_debug_spin(int microseconds, hipStream_t s);
 }  // namespace lbm
 
 using namespace lbm;
@@ -137,6 +138,40 @@ int partition(int nx, int ny, int parts, int grid_rows, int grid_cols, int &R, i
         y0 += ra[r];
     }
     return LBM_OK;
+}
+
+// Neighbours of sub-domain `id` on the R x C periodic torus of the
+// reference's partition (rank = row * C + col; the periodic halo slices of
+// StructuredGridUtils.hpp:805-851): nb[d] = the sub-domain across side d;
+// remote[d] = side d goes through the exchange (else the step kernel writes
+// the periodic image straight into the ghost ring).
+void torus_neighbours(int id, int R, int C, bool force_exchange, int nb[8], bool remote[8]) {
+    const int row = id / C, col = id % C;
+    for (int d = 0; d < 8; ++d) {
+        const int r = ((row + DIR_Y[d]) % R + R) % R;
+        const int c = ((col + DIR_X[d]) % C + C) % C;
+        nb[d] = r * C + c;
+        remote[d] = force_exchange || nb[d] != id;
+    }
+}
+
+// The ordered transfers of one sub-domain's halo exchange (format `mode`,
+// WG width `hw`): for d = E, N, W, S, NE, NW, SW, SE the send of the halo
+// leaving through side d to nb[d] (or SELF: written in place by the step
+// kernel), then the receive of ghost side OPP(d) from nb[OPP(d)].  RCCL
+// pairs the messages between two ranks purely by this posting order (one
+// ncclGroupStart/End), which is what lets extent-2 dimensions send several
+// messages to one peer.  exchange() posts exactly this list;
+// lbm_exchange_schedule exports it for host-side checking.
+std::vector<lbm_xfer> exchange_posts(int id, const int nb[8], const bool remote[8], int w, int h, int mode, int hw) {
+    std::vector<lbm_xfer> v;
+    for (int d = 0; d < 8; ++d) {
+        v.push_back(lbm_xfer{remote[d] ? LBM_XFER_SEND : LBM_XFER_SELF, d, remote[d] ? nb[d] : id, 0,
+                             msg_floats(mode, d, w, h, hw)});
+        const int e = OPP_DIR[d];
+        if (remote[e]) v.push_back(lbm_xfer{LBM_XFER_RECV, e, nb[e], 0, msg_floats(mode, e, w, h, hw)});
+    }
+    return v;
 }
 
 struct Sub {
@@ -233,6 +268,14 @@ struct lbm_handle {
     bool poison = false;          // LBM_POISON=1: fresh allocations filled with NaN bytes (read-before-write check)
     bool nan_check = false;       // LBM_NAN_CHECK=1: every run ends with a scan of the lattice for NaN / Inf
     bool tolerance = false;       // LBM_FLAG_TOLERANCE: stream kernel with the reciprocal collision (not bitwise)
+    // Ordering regression knobs (debug only, tests/test_gpu_ordering.py):
+    // LBM_DEBUG_DELAY_SUB = id of the sub-domain whose streams are stalled by
+    // LBM_DEBUG_DELAY_US before each of its compute launches;
+    // LBM_DEBUG_NO_OWN_WAIT=1 drops the LOCAL unpack's wait on the receiving
+    // sub-domain's own event (the round-4 race), so the test can show that the
+    // stall exposes the race and that the wait removes it.
+    int delay_sub = -1, delay_us = 0;
+    bool no_own_wait = false;
     int run_fused = 0, run_single = 0;  // launches of the last run: fused (spl steps) / one-step
     // Tuning knobs (environment, read at create): LBM_TWO_STEP, LBM_MAX_BLOCKS,
     // LBM_LAYOUT (rows|planar), LBM_GRAPH_STEPS, LBM_FORCE_EXCHANGE.  Defaults
@@ -326,6 +369,9 @@ struct lbm_handle {
         res_per_cu = std::min(std::max(knob("LBM_RES_PER_CU", res_per_cu), 1), 2);
         res_early_poll = knob("LBM_RES_EARLY", res_early_poll) != 0 ? 1 : 0;
         resident_max_cells = std::max(0, knob("LBM_RES_MAX_CELLS", (int)resident_max_cells));
+        delay_sub = knob("LBM_DEBUG_DELAY_SUB", -1);
+        delay_us = std::min(std::max(knob("LBM_DEBUG_DELAY_US", 0), 0), 100000);
+        no_own_wait = knob("LBM_DEBUG_NO_OWN_WAIT", 0) != 0;
         if (const char *k = knob_str("LBM_KERNEL")) {
             const std::string v(k);
             env_kernel = v == "pipeline" ? LBM_KERNEL_PIPELINE
@@ -932,12 +978,7 @@ struct lbm_handle {
             s.rect = all_rects[s.id];
             s.w = s.rect.w;
             s.h = s.rect.h;
-            for (int d = 0; d < 8; ++d) {
-                const int r = ((s.row + DIR_Y[d]) % R + R) % R;
-                const int c = ((s.col + DIR_X[d]) % C + C) % C;
-                s.nb[d] = r * C + c;
-                s.remote[d] = force_exchange || s.nb[d] != s.id;
-            }
+            torus_neighbours(s.id, R, C, force_exchange, s.nb, s.remote);
             const int gy = p.ny - 2;
             s.accel_row = (p.ny >= 2 && gy >= s.rect.y0 && gy < s.rect.y0 + s.h) ? gy - s.rect.y0 : -1;
             alloc_sub(s, obstacles);
@@ -1199,6 +1240,7 @@ struct lbm_handle {
             for (auto &s : subs) {
                 set_device(s);
                 float *cells = s.o[s.cur], *tmp = s.o[1 - s.cur];
+                debug_delay(s, s.s_comp);
                 HIP_CHECK(launch_pipe_propagate(cells, tmp, s.plane, s.pitch, s.w, s.h, s.s_comp));
                 HIP_CHECK(launch_pipe_rebound(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, s.s_comp));
                 HIP_CHECK(launch_pipe_collision(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, p.omega,
@@ -1327,18 +1369,11 @@ struct lbm_handle {
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_comm, s.ev_b, 0));
             NCCL_CHECK(ncclGroupStart());
-            for (int d = 0; d < 8; ++d) {
-                // send the halo leaving through side d to the neighbour there;
-                // receive ghost side OPP(d) from the neighbour there.  Every
-                // rank enumerates d in the same order, so repeated peers
-                // (extent-2 dimensions, or itself) match in order.
-                if (s.remote[d])
-                    NCCL_CHECK(ncclSend(s.send[d], (size_t)msg_floats(mode, d, s.w, s.h, hw), ncclFloat, s.nb[d], comm,
-                                        s.s_comm));
-                const int e = OPP_DIR[d];
-                if (s.remote[e])
-                    NCCL_CHECK(ncclRecv(s.recv[e], (size_t)msg_floats(mode, e, s.w, s.h, hw), ncclFloat, s.nb[e], comm,
-                                        s.s_comm));
+            for (const lbm_xfer &x : exchange_posts(s.id, s.nb, s.remote, s.w, s.h, mode, hw)) {
+                if (x.op == LBM_XFER_SEND)
+                    NCCL_CHECK(ncclSend(s.send[x.dir], (size_t)x.floats, ncclFloat, x.peer, comm, s.s_comm));
+                else if (x.op == LBM_XFER_RECV)
+                    NCCL_CHECK(ncclRecv(s.recv[x.dir], (size_t)x.floats, ncclFloat, x.peer, comm, s.s_comm));
             }
             NCCL_CHECK(ncclGroupEnd());
             HIP_CHECK(launch_halo_unpack(halo_args(s, target[0], mode, true), s.s_comm));
@@ -1353,7 +1388,7 @@ struct lbm_handle {
         for (size_t k = 0; k < subs.size(); ++k) {
             Sub &s = subs[k];
             set_device(s);
-            HIP_CHECK(hipStreamWaitEvent(s.s_comm, s.ev_b, 0));
+            if (!no_own_wait) HIP_CHECK(hipStreamWaitEvent(s.s_comm, s.ev_b, 0));
             for (int e = 0; e < 8; ++e) {
                 if (!s.remote[e]) continue;
                 Sub *src = local_sub(s.nb[e]);
@@ -1543,6 +1578,11 @@ struct lbm_handle {
         }
     }
 
+    // debug stall of sub-domain s's stream st (LBM_DEBUG_DELAY_SUB / _US)
+    void debug_delay(const Sub &s, hipStream_t st) const {
+        if (delay_us > 0 && s.id == delay_sub) HIP_CHECK(launch_debug_spin(delay_us, st));
+    }
+
     // launch form of a fused remainder launch of `steps` < spl steps: the
     // engine's form where it has that depth, else the shallowest that does
     int rem_form(int steps) const {
@@ -1603,6 +1643,7 @@ struct lbm_handle {
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
             wait_exchange_on(s, s.s_bnd);
+            debug_delay(s, s.s_bnd);
             HIP_CHECK(launch_part(s, s.cur, two, false, s.s_bnd, steps));
             HIP_CHECK(hipEventRecord(s.ev_b, s.s_bnd));
             HIP_CHECK(hipEventRecord(s.ev_bp[s.cur], s.s_bnd));
@@ -1612,6 +1653,7 @@ struct lbm_handle {
         for (auto &s : subs) {
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_comp, s.ev_bp[1 - s.cur], 0));  // B(t-1)
+            debug_delay(s, s.s_comp);
             HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp, steps));
             HIP_CHECK(hipEventRecord(s.ev_i, s.s_comp));
         }
@@ -1998,6 +2040,29 @@ int lbm_halo_plan(int32_t table[48]) {
         t[1] = DIR_Y[d];
         t[2] = NPLANES[d];
         for (int i = 0; i < 3; ++i) t[3 + i] = PLANES[d][i];
+    }
+    return LBM_OK;
+}
+
+int lbm_exchange_schedule(int32_t nx, int32_t ny, int32_t parts, int32_t grid_rows, int32_t grid_cols, int32_t rank,
+                          int32_t halo_mode, int32_t halo_width, int32_t force_exchange, lbm_xfer *out,
+                          int32_t max_out, int32_t *n_out) {
+    if (!n_out || (halo_mode != LBM_HALO_W1 && halo_mode != LBM_HALO_WG) || rank < 0 || rank >= parts ||
+        (halo_mode == LBM_HALO_WG && (halo_width < 1 || halo_width > MAX_GR)))
+        return LBM_E_INVALID;
+    int R = 0, C = 0;
+    std::vector<lbm_rect> rects;
+    const int rc = partition(nx, ny, parts, grid_rows, grid_cols, R, C, rects);
+    if (rc != LBM_OK) return rc;
+    int nb[8];
+    bool remote[8];
+    torus_neighbours(rank, R, C, force_exchange != 0, nb, remote);
+    const auto v = exchange_posts(rank, nb, remote, rects[rank].w, rects[rank].h, halo_mode,
+                                  halo_mode == LBM_HALO_WG ? halo_width : 1);
+    *n_out = (int32_t)v.size();
+    if (out) {
+        if (max_out < (int32_t)v.size()) return LBM_E_INVALID;
+        for (size_t i = 0; i < v.size(); ++i) out[i] = v[i];
     }
     return LBM_OK;
 }

@@ -482,6 +482,22 @@ hipError_t launch_step(const StepArgs &a, int blocks, bool vec4, bool reduce, hi
     return hipGetLastError();
 }
 
+// Debug-only stall (LBM_DEBUG_DELAY_*, engines' ordering regression tests):
+// one lane spins on the 100 MHz constant clock for `ticks` ticks.  Queued on
+// one sub-domain's stream it holds that stream back while the other
+// sub-domains run ahead, which makes a missing cross-stream wait show every
+// time instead of once in a few hundred runs.
+__global__ void debug_spin(long long ticks) {
+    const long long end = (long long)wall_clock64() + ticks;
+    while ((long long)wall_clock64() < end) __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_debug_spin(int microseconds, hipStream_t s) {
+    if (microseconds <= 0) return hipSuccess;
+    hipLaunchKernelGGL(debug_spin, dim3(1), dim3(1), 0, s, (long long)microseconds * 100);
+    return hipGetLastError();
+}
+
 hipError_t launch_finalize(const float *partials, float *av_local, int *ctl, hipStream_t s) {
     hipLaunchKernelGGL(finalize_av, dim3(1), dim3(BLOCK), 0, s, partials, av_local, ctl);
     return hipGetLastError();

@@ -19,17 +19,20 @@ PKG_ROOT = Path(__file__).resolve().parent.parent          # lbm-graphcore_amd/
 LIB_PATH = Path(os.environ.get("LBM_HIP_LIB", PKG_ROOT / "build" / "liblbm_hip.so"))
 
 Q = 9
-ABI_VERSION = 4          # LBM_ABI_VERSION in include/lbm_hip.h
+ABI_VERSION = 5          # LBM_ABI_VERSION in include/lbm_hip.h
 
 LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
 TRANSPORT_LOCAL, TRANSPORT_RCCL = 0, 1
 KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4, KERNEL_STEP2, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PIPELINE = range(7)
 FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP, FLAG_TOLERANCE = 1, 2, 4
+XFER_SEND, XFER_RECV, XFER_SELF = 0, 1, 2
+HALO_W1, HALO_WG = 1, 2
 
 # every symbol include/lbm_hip.h declares
 EXPORTED = [
-    "lbm_abi_version", "lbm_partition", "lbm_halo_plan", "lbm_device_count", "lbm_rccl_unique_id",
+    "lbm_abi_version", "lbm_partition", "lbm_halo_plan", "lbm_exchange_schedule", "lbm_device_count",
+    "lbm_rccl_unique_id",
     "lbm_create", "lbm_create_ex", "lbm_load_cells", "lbm_init_equilibrium",
     "lbm_run", "lbm_run_steps", "lbm_store", "lbm_load_cells_local", "lbm_store_local", "lbm_local_cells",
     "lbm_last_run_seconds",
@@ -40,7 +43,8 @@ EXPORTED = [
 # every symbol include/lbm3d_hip.h declares (D3Q19 extension)
 EXPORTED3D = [
     "lbm3d_create", "lbm3d_init_equilibrium", "lbm3d_load_cells", "lbm3d_run_steps", "lbm3d_store",
-    "lbm3d_last_run_seconds", "lbm3d_total_free_cells", "lbm3d_local_slabs", "lbm3d_last_error", "lbm3d_destroy",
+    "lbm3d_last_run_seconds", "lbm3d_total_free_cells", "lbm3d_local_slabs", "lbm3d_exchange_schedule",
+    "lbm3d_last_error", "lbm3d_destroy",
 ]
 Q3 = 19
 
@@ -92,6 +96,12 @@ class Rect(ctypes.Structure):
     _fields_ = [("x0", ctypes.c_int32), ("y0", ctypes.c_int32), ("w", ctypes.c_int32), ("h", ctypes.c_int32)]
 
 
+class Xfer(ctypes.Structure):
+    """lbm_xfer (include/lbm_hip.h): one post of a halo exchange."""
+    _fields_ = [("op", ctypes.c_int32), ("dir", ctypes.c_int32), ("peer", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("floats", ctypes.c_int64)]
+
+
 _lib = None
 
 
@@ -125,6 +135,9 @@ def load_library() -> ctypes.CDLL:
         "lbm_abi_version": ([], i32),
         "lbm_partition": ([i32, i32, i32, i32, i32, i32p, i32p, ctypes.POINTER(Rect)], ctypes.c_int),
         "lbm_halo_plan": ([i32p], ctypes.c_int),
+        "lbm_exchange_schedule": ([i32, i32, i32, i32, i32, i32, i32, i32, i32, ctypes.POINTER(Xfer), i32, i32p],
+                                  ctypes.c_int),
+        "lbm3d_exchange_schedule": ([i32, i32, i32, i32, i32, i32, ctypes.POINTER(Xfer), i32, i32p], ctypes.c_int),
         "lbm_device_count": ([], i32),
         "lbm_rccl_unique_id": ([u8p], ctypes.c_int),
         "lbm_create": ([ctypes.POINTER(Params), u8p, i32, ctypes.POINTER(H)], ctypes.c_int),
@@ -195,6 +208,32 @@ def halo_plan():
         dx, dy, n = t[6 * d], t[6 * d + 1], t[6 * d + 2]
         out.append((dx, dy, [t[6 * d + 3 + i] for i in range(n)]))
     return out
+
+
+def exchange_schedule(nx: int, ny: int, parts: int, rank: int, mode: int = HALO_WG, halo_width: int = 1,
+                      grid_rows: int = 0, grid_cols: int = 0, force_exchange: bool = False):
+    """The engine's own ordered halo-exchange posts for `rank` (lbm_exchange_schedule):
+    [(op, dir, peer, floats), ...] with op XFER_SEND / XFER_RECV / XFER_SELF."""
+    L = load_library()
+    buf = (Xfer * 32)()
+    n = ctypes.c_int32()
+    rc = L.lbm_exchange_schedule(nx, ny, parts, grid_rows, grid_cols, rank, mode, halo_width, int(force_exchange),
+                                 buf, 32, ctypes.byref(n))
+    if rc != LBM_OK:
+        raise LbmError(rc, f"lbm_exchange_schedule({nx}, {ny}, {parts}, rank {rank}) failed")
+    return [(x.op, x.dir, x.peer, x.floats) for x in buf[:n.value]]
+
+
+def exchange_schedule3d(nx: int, ny: int, nz: int, parts: int, rank: int, planes: int):
+    """The D3Q19 engine's ordered z-slab exchange posts (lbm3d_exchange_schedule);
+    dir 0 = +z (up), 1 = -z (down)."""
+    L = load_library()
+    buf = (Xfer * 4)()
+    n = ctypes.c_int32()
+    rc = L.lbm3d_exchange_schedule(nx, ny, nz, parts, rank, planes, buf, 4, ctypes.byref(n))
+    if rc != LBM_OK:
+        raise LbmError(rc, f"lbm3d_exchange_schedule({nx}, {ny}, {nz}, {parts}, rank {rank}) failed")
+    return [(x.op, x.dir, x.peer, x.floats) for x in buf[:n.value]]
 
 
 def device_count() -> int:

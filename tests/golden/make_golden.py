@@ -11,6 +11,14 @@ container, where /root/reference exists; the GPU box only reads the output).
                         whether the reference's own LastChance binary produced
                         byte-identical av_vels.dat / final_state.dat text
   oracle/<grid>.av_vels.npy.gz   oracle av_vels (float32) for every step
+  oracle/<grid>.final_state_pressure.npy.gz
+                      the pressure column of the oracle's final_state.dat
+                      (float32[ny][nx], writeResults' arithmetic) -- the
+                      second file of the check.py gate on the grids whose
+                      check/*.final_state.dat the reference does not ship
+                      (256x256, 1024x1024: /root/reference/.MISSING_LARGE_BLOBS);
+                      the oracle's final_state text is byte-identical to the
+                      reference binary's on every grid (oracle/<grid>.json)
   small.npz           full lattices after 1, 2 and 10 steps on small synthetic
                       problems (walls, interior wall, ragged widths, 1-row grid)
   oracle_pipe/<grid>.json, .av_vels.npy.gz
@@ -134,6 +142,29 @@ def run_pipe_grid(grid: str) -> dict:
     return out
 
 
+def write_final_state_fixture(grid: str, threads: int = 8) -> dict:
+    """Pressure column of the oracle's final_state at full maxIters.  The
+    lattice comes from the multi-threaded oracle (bitwise equal to run());
+    its sha256 must equal the manifest's, so the fixture is pinned to the
+    same lattice whose final_state.dat text matched the reference binary's."""
+    pf, of = grid_files(grid)
+    p = lio.Params.from_file(str(pf))
+    obst = lio.read_obstacles(p.nx, p.ny, str(of))
+    cells, _ = oracle.run_mt(p, obst, p.max_iters, threads)
+    man_path = GOLD / "oracle" / f"{grid}.json"
+    man = json.loads(man_path.read_text())
+    if lattice_sha256(cells) != man["final_f_sha256"]:
+        raise RuntimeError(f"{grid}: oracle_run_mt lattice differs from the manifest's sha256")
+    _, _, _, pr = lio.macroscopic(p, obst, cells)
+    pr = np.ascontiguousarray(pr, dtype=np.float32)
+    buf = _io.BytesIO()
+    np.save(buf, pr)
+    (GOLD / "oracle" / f"{grid}.final_state_pressure.npy.gz").write_bytes(gzip.compress(buf.getvalue(), 9))
+    man["final_state_pressure_sha256"] = hashlib.sha256(pr.tobytes()).hexdigest()
+    man_path.write_text(json.dumps(man, indent=1) + "\n")
+    return {"grid": grid, "pressure_sha256": man["final_state_pressure_sha256"]}
+
+
 def small_problems():
     """Small synthetic problems for step-level bitwise vectors."""
     probs = []
@@ -195,9 +226,15 @@ def main():
     ap.add_argument("--jobs", type=int, default=4)
     ap.add_argument("--skip-small", action="store_true")
     ap.add_argument("--pipe-grids", default="", help="also write oracle_pipe/ manifests for these grids")
+    ap.add_argument("--fs-grids", default="",
+                    help="only (re)write oracle/<grid>.final_state_pressure.npy.gz for these grids")
     a = ap.parse_args()
     oracle.build()
     (GOLD / "oracle").mkdir(exist_ok=True)
+    if a.fs_grids:
+        for g in a.fs_grids.split(","):
+            print(json.dumps(write_final_state_fixture(g)))
+        return
     if not a.skip_small:
         make_small()
         print("small.npz written")
@@ -207,6 +244,9 @@ def main():
     with ProcessPoolExecutor(max_workers=a.jobs) as ex:
         for res in ex.map(run_grid, grids):
             print(json.dumps(res))
+    for g in grids:
+        print(json.dumps(write_final_state_fixture(g)))
+    with ProcessPoolExecutor(max_workers=a.jobs) as ex:
         for res in ex.map(run_pipe_grid, pipe):
             print(json.dumps(res))
 

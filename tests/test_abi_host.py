@@ -30,7 +30,7 @@ def header_symbols(name="lbm_hip.h", prefix="lbm_"):
 def test_library_exports_every_d3q19_symbol():
     L = native.load_library()
     syms = header_symbols("lbm3d_hip.h", "lbm3d_")
-    assert len(syms) == 10
+    assert len(syms) == 11
     assert sorted(native.EXPORTED3D) == syms
     out = subprocess.run(["nm", "-D", "--defined-only", str(native.LIB_PATH)], capture_output=True, text=True,
                          check=True).stdout
@@ -50,7 +50,7 @@ def test_library_exports_every_declared_symbol():
                          check=True).stdout
     for s in syms:
         assert re.search(rf"\bT {s}\b", out), s
-    assert L.lbm_abi_version() == 4
+    assert L.lbm_abi_version() == 5
 
 
 def test_stale_library_is_refused(monkeypatch):

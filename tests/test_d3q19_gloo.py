@@ -4,7 +4,9 @@ Mirrors the engine's multi-rank D3Q19 path (lbm-graphcore_amd/csrc/lbm3d.hip):
 round-robin z extents, and after every step each rank sends its top plane's
 speeds 9..13 (c_z = +1, one contiguous block) up and its bottom plane's speeds
 14..18 down, posted in the same order as the RCCL group (send up, send down,
-receive from below, receive from above).  The step is the CPU restatement on
+receive from below, receive from above) -- the list comes from the library
+(lbm3d_exchange_schedule, what the RCCL exchange posts) and is posted
+untagged.  The step is the CPU restatement on
 the ghosted slab; ghost-plane speeds the plan does not deliver are NaN, so a
 missing or misrouted population shows up.  The gathered lattice must equal the
 single-domain restatement bit for bit.  (Parity unpinned upstream: the
@@ -51,6 +53,7 @@ def _worker(rank, world, port, result_q):
     os.environ["MASTER_PORT"] = str(port)
     import torch
     import torch.distributed as dist
+    from lbm_amd import native
     from oracle import oracle
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -67,10 +70,18 @@ def _worker(rank, world, port, result_q):
             g[-1] = np.nan
             below = torch.empty((p.ny, p.nx, 5), dtype=torch.float32)
             above = torch.empty((p.ny, p.nx, 5), dtype=torch.float32)
-            reqs = [dist.isend(torch.from_numpy(np.ascontiguousarray(g[n][..., UP])), dst=up, tag=0),
-                    dist.isend(torch.from_numpy(np.ascontiguousarray(g[1][..., DOWN])), dst=down, tag=1),
-                    dist.irecv(below, src=down, tag=0),
-                    dist.irecv(above, src=up, tag=1)]
+            reqs = []
+            # the engine's own posting list (lbm3d_exchange_schedule, one-step
+            # face exchange), untagged: with two slabs up == down and gloo pairs
+            # the two messages by order, as RCCL does
+            for op, d, peer, floats in native.exchange_schedule3d(p.nx, p.ny, p.nz, world, rank, 1):
+                assert peer == (up if d == 0 else down)
+                assert floats == 5 * p.ny * ((p.nx + 15) // 16 * 16)  # the engine's padded speed planes
+                if op == native.XFER_SEND:
+                    face = g[n][..., UP] if d == 0 else g[1][..., DOWN]
+                    reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(face)), dst=peer))
+                else:
+                    reqs.append(dist.irecv(below if d == 1 else above, src=peer))
             for r in reqs:
                 r.wait()
             g[0][..., UP] = below.numpy()

@@ -3,8 +3,10 @@
 Each rank owns the sub-domain the library's own partition rule assigns it
 (lbm_partition, StructuredGridUtils.hpp:472-561 semantics) and exchanges a
 one-cell halo every step following the library's own halo plan
-(lbm_halo_plan: which populations leave through which side, and the
-receive-side pairing the RCCL transport uses).  The step itself is the CPU
+(lbm_halo_plan: which populations leave through which side) and the
+engine's own ordered posting list (lbm_exchange_schedule, W1 format: the
+sends and receives exchange() posts in one RCCL group), untagged, so gloo
+pairs them by order exactly as RCCL does.  The step itself is the CPU
 oracle on the ghosted block.  Ghost planes NOT covered by the plan are
 poisoned with NaN, so a missing population would show up.  After N steps the
 gathered lattice must equal the single-domain oracle bit for bit.
@@ -21,6 +23,7 @@ import pytest
 from conftest import PKG, ROOT
 
 STEPS = 6
+OPP = [2, 3, 0, 1, 6, 7, 4, 5]   # E N W S NE NW SW SE -> opposite side
 
 
 def _problem():
@@ -63,10 +66,6 @@ def _worker(rank, world, port, result_q):
         R, C, rects = native.partition(p.nx, p.ny, world)
         plan = native.halo_plan()
         x0, y0, w, h = rects[rank]
-        row, col = rank // C, rank % C
-
-        def nb(dx, dy):
-            return ((row + dy) % R) * C + (col + dx) % C
 
         # the one-time accelerate is pointwise on row ny-2 (LastChance.cpp:161-183):
         # apply it to the initial state, then decompose
@@ -84,27 +83,31 @@ def _worker(rank, world, port, result_q):
             g[:, 0, :] = np.nan
             g[:, -1, :] = np.nan
             reqs, bufs = [], []
-            # post receives: ghost side OPP(d) from the neighbour there (engine order)
-            for i, (dx, dy, planes) in enumerate(plan):
-                src = nb(-dx, -dy)
-                if src == rank:
-                    continue
-                ys, xs = _ranges(-dx, -dy, w, h, True)
-                shape = g[ys, xs][..., planes].shape
-                buf = torch.empty(shape, dtype=torch.float32)
-                bufs.append((ys, xs, planes, buf))
-                reqs.append(dist.irecv(buf, src=src, tag=i))
-            for i, (dx, dy, planes) in enumerate(plan):
-                ys, xs = _ranges(dx, dy, w, h, False)
-                data = np.ascontiguousarray(g[ys, xs][..., planes])
-                dst = nb(dx, dy)
-                if dst == rank:  # periodic wrap inside this block
+            # the engine's own posting list for one-step launches (W1 halo:
+            # lbm_exchange_schedule, what exchange() posts in one RCCL group),
+            # in that order and with no tags: messages to one peer match by order
+            for op, d, peer, floats in native.exchange_schedule(p.nx, p.ny, world, rank, native.HALO_W1):
+                dx, dy, planes = plan[d]
+                if op == native.XFER_SELF:   # periodic wrap inside this block
+                    assert peer == rank
+                    ys, xs = _ranges(dx, dy, w, h, False)
                     gy, gx = _ranges(-dx, -dy, w, h, True)
                     sub = g[gy, gx]
-                    sub[..., planes] = data
+                    sub[..., planes] = g[ys, xs][..., planes]
                     g[gy, gx] = sub
-                else:
-                    reqs.append(dist.isend(torch.from_numpy(data), dst=dst, tag=i))
+                elif op == native.XFER_SEND:  # populations leaving through side d
+                    ys, xs = _ranges(dx, dy, w, h, False)
+                    data = np.ascontiguousarray(g[ys, xs][..., planes])
+                    assert data.size == floats
+                    reqs.append(dist.isend(torch.from_numpy(data), dst=peer))
+                else:                         # ghost side d: the neighbour's populations leaving through OPP(d)
+                    odx, ody, oplanes = plan[OPP[d]]
+                    ys, xs = _ranges(dx, dy, w, h, True)
+                    shape = g[ys, xs][..., oplanes].shape
+                    assert int(np.prod(shape)) == floats
+                    buf = torch.empty(shape, dtype=torch.float32)
+                    bufs.append((ys, xs, oplanes, buf))
+                    reqs.append(dist.irecv(buf, src=peer))
             for r in reqs:
                 r.wait()
             for ys, xs, planes, buf in bufs:

@@ -15,8 +15,7 @@ import json
 import numpy as np
 import pytest
 
-from conftest import GOLD, GRIDS, load_problem, oracle_av_vels, oracle_manifest, small_problems
-from lbm_amd import check as lcheck
+from conftest import GOLD, GRIDS, check_gate, load_problem, oracle_av_vels, oracle_manifest, small_problems
 from lbm_amd import io as lio
 from oracle import oracle
 
@@ -160,10 +159,12 @@ def test_decomposed_small_ragged(gpu_lib, parts, mode):
 # ------------------------------------------------ reference grids ----
 
 @pytest.mark.parametrize("grid", GRIDS)
-@pytest.mark.parametrize("mode", ["vec4", "step2", "stream4", "stream5", "resident"])
+@pytest.mark.parametrize("mode", ["scalar", "vec4", "step2", "stream4", "stream5", "stream6", "resident"])
 def test_reference_grid_full_run(gpu_lib, grid, mode, tmp_path):
     """Full maxIters run: final lattice bitwise == oracle (sha256), av_vels ~ oracle,
-    and the reference gate (check.py, 1 %) against check/*.dat passes."""
+    and the reference gate with BOTH files (check.py, 1 %) passes -- final_state
+    against check/*.dat where the reference ships it, else the oracle's
+    (conftest.reference_final_state)."""
     p, obst = load_problem(grid)
     m = oracle_manifest(grid)
     with gpu_lib.Engine(p, obst, **mode_kw(gpu_lib, mode)) as e:
@@ -175,15 +176,10 @@ def test_reference_grid_full_run(gpu_lib, grid, mode, tmp_path):
     assert sha(cells) == m["final_f_sha256"]
     np.testing.assert_allclose(av, oracle_av_vels(grid), rtol=AV_RTOL)
     assert lio.reynolds_number(p, float(av[-1])) == pytest.approx(m["reynolds_last_av"], rel=AV_RTOL)
-    lio.write_average_velocities(str(tmp_path / "av_vels.dat"), av)
-    ref_av = lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz")
-    assert abs(lcheck.diff_values(ref_av, lcheck.load_av_vels(tmp_path / "av_vels.dat"))["max_diff_pcnt"]) < 1.0
-    fs_fixture = GOLD / "check" / f"{grid}.final_state.dat.gz"
-    if fs_fixture.exists():
-        lio.write_results(str(tmp_path / "final_state.dat"), p, obst, cells)
-        res = lcheck.compare(GOLD / "check" / f"{grid}.av_vels.dat.gz", fs_fixture, tmp_path / "av_vels.dat",
-                             tmp_path / "final_state.dat", 1.0)
-        assert res["passed"], res
+    res = check_gate(grid, p, obst, cells, av, tmp_path)
+    assert res["passed"], res
+    if res["fs_source"] == "oracle final_state":  # bitwise lattice -> bitwise pressure column
+        assert res["fs"]["max_diff_pcnt"] == pytest.approx(0.0, abs=1e-9)
 
 
 def test_determinism_and_rerun(gpu_lib):
@@ -600,10 +596,10 @@ def test_pipeline_decomposed_bitwise(gpu_lib, parts, grid):
     np.testing.assert_allclose(av, ref_av, rtol=1e-5)
 
 
-@pytest.mark.parametrize("grid", ["128x128", "128x256", "256x256"])
+@pytest.mark.parametrize("grid", GRIDS)
 def test_pipeline_reference_grid_full_run(gpu_lib, grid, tmp_path):
     """Full maxIters: final lattice sha256 == the pipeline oracle's, av_vels ~ oracle,
-    and the reference gate (check.py vs check/*.dat) passes."""
+    and the two-file reference gate (check.py, 1 %) passes."""
     p, obst = load_problem(grid)
     m = pipe_manifest(grid)
     with gpu_lib.Engine(p, obst, kernel=gpu_lib.KERNEL_PIPELINE) as e:
@@ -613,10 +609,8 @@ def test_pipeline_reference_grid_full_run(gpu_lib, grid, tmp_path):
     assert sha(cells) == m["final_f_sha256"]
     ref_av = np.load(io.BytesIO(gzip.decompress((GOLD / "oracle_pipe" / f"{grid}.av_vels.npy.gz").read_bytes())))
     np.testing.assert_allclose(av, ref_av, rtol=AV_RTOL)
-    lio.write_average_velocities(str(tmp_path / "av_vels.dat"), av)
-    d = lcheck.diff_values(lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz"),
-                           lcheck.load_av_vels(tmp_path / "av_vels.dat"))
-    assert abs(d["max_diff_pcnt"]) < 1.0
+    res = check_gate(grid, p, obst, cells, av, tmp_path)
+    assert res["passed"], res
 
 
 # ------------------------------------- wide decomposed x bands (stream) ----

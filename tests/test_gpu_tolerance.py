@@ -3,8 +3,11 @@ collision (lbm_packed.hpp collide2t) is not bitwise equal to the reference's
 LastChance.cpp:226-262 arithmetic; north_star allows "a stated fp32
 tolerance".  What is stated and checked here:
 
-  * the reference gate: check.py (1 %) against check/*.dat on all four
-    reference grids at full maxIters;
+  * full maxIters on all four reference grids (20000 steps at 1024^2): every
+    population within TOL_POP_FULL relative of the oracle's final lattice,
+    av_vels within TOL_AV_FULL, and the two-file check.py gate (1 %) --
+    final_state against check/*.dat where the reference ships it, else the
+    oracle's final_state (conftest.reference_final_state);
   * every population within TOL_POP relative of the oracle after 100 steps at
     8192^2 (BASELINE config 3, the bench workload), av_vels within TOL_AV;
   * the tolerance kernel's own results do not depend on the decomposition:
@@ -13,18 +16,39 @@ tolerance".  What is stated and checked here:
 """
 from __future__ import annotations
 
+import functools
+import hashlib
+import os
+
 import numpy as np
 import pytest
 
-from conftest import GOLD, GRIDS, load_problem, oracle_av_vels
-from lbm_amd import check as lcheck
+from conftest import GRIDS, check_gate, load_problem, oracle_av_vels, oracle_manifest
 from lbm_amd import io as lio
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-TOL_POP = 2e-5   # max |f_gpu - f_oracle| / |f_oracle| over every population
+TOL_POP = 2e-5   # max |f_gpu - f_oracle| / |f_oracle| over every population (<= 100 steps)
 TOL_AV = 2e-4    # av_vels, relative
+# full reference runs (maxIters: 40000 steps at 128^2 / 128x256, 80000 at
+# 256^2, 20000 at 1024^2): the stated bound for long runs (include/lbm_hip.h
+# LBM_FLAG_TOLERANCE).  Measured on MI355X (profiles/r05/gate/): populations
+# 4.3e-4 / 5.6e-4 / 8.5e-4 / 4.0e-4, av_vels 2.4e-4 / 3.8e-4 / 8.7e-4 / 3.9e-4
+# -- the same for the stream and the resident kernel (one collision).
+TOL_POP_FULL = 2e-3
+TOL_AV_FULL = 2e-3
+
+
+@functools.lru_cache(maxsize=4)
+def _oracle_final(grid):
+    """The oracle's final lattice at full maxIters on the host's cores (bitwise
+    equal to oracle.run: its sha256 must match the committed manifest)."""
+    p, obst = load_problem(grid)
+    cells, _ = oracle.run_mt(p, obst, p.max_iters, min(16, os.cpu_count() or 1))
+    assert hashlib.sha256(np.ascontiguousarray(cells, "<f4").tobytes()).hexdigest() == \
+        oracle_manifest(grid)["final_f_sha256"]
+    return cells
 
 
 def _tol_kw(gpu_lib, **kw):
@@ -46,8 +70,10 @@ def _rel(a, b, chunk=1 << 26):
 @pytest.mark.parametrize("grid", GRIDS)
 def test_tolerance_reference_grids_check_py(gpu_lib, grid, kernel, tmp_path):
     """Full maxIters with the tolerance collision (stream kernel, and the packed
-    resident tiles AUTO picks for these grids): check.py passes, av_vels close
-    to the oracle's."""
+    resident tiles AUTO picks for these grids): every population within
+    TOL_POP_FULL of the oracle's final lattice, av_vels close to the oracle's,
+    and the two-file check.py gate passes (final_state against check/*.dat
+    where the reference ships it, else the oracle's final_state)."""
     p, obst = load_problem(grid)
     kw = dict(kernel=gpu_lib.KERNEL_STREAM if kernel == "stream" else gpu_lib.KERNEL_RESIDENT,
               flags=gpu_lib.FLAG_TOLERANCE)
@@ -57,18 +83,16 @@ def test_tolerance_reference_grids_check_py(gpu_lib, grid, kernel, tmp_path):
         e.run()
         cells, av = e.store()
     assert np.isfinite(cells).all()
+    ref = _oracle_final(grid)
+    dpop = _rel(cells, ref)
     dev = float(np.max(np.abs(av - oracle_av_vels(grid)) / np.abs(oracle_av_vels(grid))))
-    print(f"{grid} {kernel}: av_vels max relative deviation from the oracle {dev:.3e}")
-    assert dev < TOL_AV * 10
-    lio.write_average_velocities(str(tmp_path / "av_vels.dat"), av)
-    ref_av = lcheck.load_av_vels(GOLD / "check" / f"{grid}.av_vels.dat.gz")
-    assert abs(lcheck.diff_values(ref_av, lcheck.load_av_vels(tmp_path / "av_vels.dat"))["max_diff_pcnt"]) < 1.0
-    fs = GOLD / "check" / f"{grid}.final_state.dat.gz"
-    if fs.exists():
-        lio.write_results(str(tmp_path / "final_state.dat"), p, obst, cells)
-        res = lcheck.compare(GOLD / "check" / f"{grid}.av_vels.dat.gz", fs, tmp_path / "av_vels.dat",
-                             tmp_path / "final_state.dat", 1.0)
-        assert res["passed"], res
+    res = check_gate(grid, p, obst, cells, av, tmp_path)
+    print(f"{grid} {kernel} tolerance, {p.max_iters} steps: populations max relative deviation {dpop:.3e}, "
+          f"av_vels {dev:.3e}, check.py av {res['av']['max_diff_pcnt']:.3e} % "
+          f"final_state {res['fs']['max_diff_pcnt']:.3e} % ({res['fs_source']})")
+    assert dpop < TOL_POP_FULL
+    assert dev < TOL_AV_FULL
+    assert res["passed"], res
 
 
 def test_tolerance_8192_vs_oracle(gpu_lib):

@@ -12,7 +12,8 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from conftest import GOLD, load_problem, oracle_av_vels, oracle_manifest, small_problems
+from conftest import (GOLD, load_problem, oracle_av_vels, oracle_manifest, oracle_pressure, reference_final_state,
+                      small_problems)
 from lbm_amd import check as lcheck
 from lbm_amd import io as lio
 from oracle import oracle
@@ -129,6 +130,28 @@ def test_oracle_matches_reference_fixtures(grid, tmp_path):
     from golden.make_golden import lattice_sha256
     assert lattice_sha256(cells) == m["final_f_sha256"]
     assert np.array_equal(av, oracle_av_vels(grid))
+    # the committed final_state pressure fixture is this lattice's pressure column
+    _, _, _, pr = lio.macroscopic(p, obst, cells)
+    assert np.array_equal(pr, oracle_pressure(grid))
+
+
+@pytest.mark.parametrize("grid", ["128x128", "128x256", "256x256", "1024x1024"])
+def test_final_state_fixture_gate(grid, tmp_path):
+    """The second file of the two-file gate on every grid.  Where the reference
+    ships check/<grid>.final_state.dat, the oracle's pressure fixture passes
+    check.py against it; everywhere, the fixture's sha256 is the manifest's."""
+    import hashlib
+    pr = oracle_pressure(grid)
+    m = oracle_manifest(grid)
+    assert pr.dtype == np.float32 and pr.shape == (m["ny"], m["nx"])
+    assert hashlib.sha256(pr.tobytes()).hexdigest() == m["final_state_pressure_sha256"]
+    ref_fs, src = reference_final_state(grid)
+    if src == "reference check/":
+        ref = lcheck.load_final_state(ref_fs)
+        d = lcheck.diff_values(ref[:, 2], pr.ravel().astype(np.float64))
+        assert abs(d["max_diff_pcnt"]) < 0.1, d
+    else:
+        assert grid in ("256x256", "1024x1024")
 
 
 @pytest.mark.parametrize("grid", ["128x128", "128x256", "256x256", "1024x1024"])

@@ -6,12 +6,15 @@ halo: S x len strips for the four sides, S x S blocks for the corners) once
 per launch, and RCCL matches the messages between two ranks purely by posting
 order: the engine posts, for d = E, N, W, S, NE, NW, SW, SE, the send of the
 strip leaving through d to the neighbour there, then the receive of ghost
-side OPP(d) from the neighbour there (lbm_engine.hip exchange(), the
-ncclGroupStart/End block).  Here every rank does the same with gloo isend /
+side OPP(d) from the neighbour there (lbm_engine.hip exchange_posts, posted
+by exchange() in one ncclGroupStart/End block).  Here every rank posts the
+same list with gloo isend /
 irecv and NO tags (one default tag: messages to one peer match in order),
 then advances S steps on its ghosted block with the CPU oracle (the ring
 shrinks by one cell per step), and the gathered lattice must equal the
-single-domain oracle bit for bit.  Extent-2 dimensions (1x2, 2x1, 2x2, 2x4)
+single-domain oracle bit for bit.  The posts come from the library itself
+(lbm_exchange_schedule, the list exchange() iterates), not from a Python
+restatement of the order.  Extent-2 dimensions (1x2, 2x1, 2x2, 2x4)
 send several messages to the same peer per exchange, which is exactly where
 order matching matters; 8x1 and 2x4 are the bench's two 8-GPU layouts.
 Reference side of the contract: the per-step stitched halos of
@@ -122,12 +125,6 @@ def _worker(rank, world, grid, port, result_q):
         R, C, rects = native.partition(p.nx, p.ny, world, *grid)
         assert (R, C) == grid
         x0, y0, w, h = rects[rank]
-        row, col = rank // C, rank % C
-
-        def nb(d):
-            dx, dy = DIRS[d]
-            return ((row + dy) % R) * C + (col + dx) % C
-
         cells_acc = cells0.copy()
         oracle.accelerate(p, cells_acc, obst)
         # rank 0 scatters the blocks (lbm_load_cells_local's host side)
@@ -147,22 +144,28 @@ def _worker(rank, world, grid, port, result_q):
                 g = np.full((h + 2 * S, w + 2 * S, 9), np.nan, np.float32)
                 g[S:S + h, S:S + w] = blk
                 reqs, recvs = [], []
-                for d in range(8):   # engine order: send(d), then recv(OPP(d)); no tags
+                # the engine's own posting list (lbm_exchange_schedule = what
+                # exchange() posts inside one ncclGroupStart/End), no tags
+                for op, d, peer, floats in native.exchange_schedule(p.nx, p.ny, world, rank, native.HALO_WG, S,
+                                                                    R, C):
                     dx, dy = DIRS[d]
-                    if nb(d) == rank:   # periodic wrap inside this block: write the image directly
+                    if op == native.XFER_SELF:   # periodic wrap inside this block: the image in place
+                        assert peer == rank
                         gys, gxs = _ghost(S, w, h, -dx, -dy)
                         eys, exs = _edge(g, S, w, h, dx, dy)
                         g[gys, gxs] = g[eys, exs]
-                    else:
+                    elif op == native.XFER_SEND:
                         eys, exs = _edge(g, S, w, h, dx, dy)
-                        reqs.append(dist.isend(torch.from_numpy(_pack(g, eys, exs, d)), dst=nb(d)))
-                    e = OPP[d]
-                    if nb(e) != rank:
-                        gys, gxs = _ghost(S, w, h, *DIRS[e])
-                        shape = _pack(g, gys, gxs, d).shape  # the neighbour's strip of direction OPP(e) = d
+                        msg = _pack(g, eys, exs, d)
+                        assert msg.size == floats, (d, msg.shape, floats)
+                        reqs.append(dist.isend(torch.from_numpy(msg), dst=peer))
+                    else:                        # ghost side d, the neighbour's strip of direction OPP(d)
+                        gys, gxs = _ghost(S, w, h, dx, dy)
+                        shape = _pack(g, gys, gxs, OPP[d]).shape
+                        assert int(np.prod(shape)) == floats, (d, shape, floats)
                         buf = torch.empty(shape, dtype=torch.float32)
-                        recvs.append((gys, gxs, d, buf))
-                        reqs.append(dist.irecv(buf, src=nb(e)))
+                        recvs.append((gys, gxs, OPP[d], buf))
+                        reqs.append(dist.irecv(buf, src=peer))
                 for r_ in reqs:
                     r_.wait()
                 for gys, gxs, d, buf in recvs:
