@@ -11,7 +11,8 @@ reciprocal of rho per cell, within the tolerance the line states, north_star's
 "within a stated fp32 tolerance") or bitwise (every population identical to
 the reference arithmetic); the other one runs the same workload in aux.
 Steps per launch: the S that finishes K steps soonest by the measured launch
-times (pick_spl; a remainder of >= 2 steps is one fused launch), reported in
+times (pick_spl over calibrate_launch_ms: every S timed on the box at bench
+start, untimed; a remainder of >= 2 steps is one fused launch), reported in
 launches.plan.
 
 One "step" = one fused lattice update of every cell (pull-stream, rebound /
@@ -57,8 +58,11 @@ profile of this workload + kernel exists, else null.  effective_gbs = 72 B x
 cell updates / s (SURVEY 8(d)'s MLUPS x 72 B form), which exceeds the HBM
 peak once temporal blocking pays.  roofline.valu = VALU instructions per
 launch and the VALU pipe's busy fraction from the SQ pass of the same profile
-(tools/pmc_traffic.py --sq); roofline.bound = "valu" where that pipe is busy
->= 75 % of the SIMD cycles (the bitwise kernel), else "hbm".
+(tools/pmc_traffic.py --sq).  roofline.bound: "hbm" when frac or
+frac_counter_bytes (the PMC bytes over the same launch time) reaches 0.75,
+"valu" when frac_valu_issue (VALU busy in quad-cycle units) does -- the larger
+wins -- and "latency" when none does (the launch waits on loads, LDS and
+dependency chains rather than saturating either pipe).
 
 cpu_baseline: the reference's main/LbmCpu.cpp as committed (north_star: "next
 to LbmCpu.cpp timed on the same box's host cores"), built from its source by
@@ -256,29 +260,42 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
     p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
     obst = synthetic_obstacles(n, n)
     numerics = "tolerance" if flags & native.FLAG_TOLERANCE else "bitwise"
-    kw = dict(devices=[local_rank], flags=flags, steps_per_launch=pick_spl(steps, 0, numerics))
+    cal = next((v for (_, _, nm), v in _LAUNCH_CAL.items() if nm == numerics), None)
+    kw = dict(devices=[local_rank], flags=flags, steps_per_launch=pick_spl(steps, 0, numerics, table=cal))
     if dist_on:
         box = [native.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         kw.update(parts=world, transport=native.TRANSPORT_RCCL, rank=rank, world=world, unique_id=box[0])
         if slabs:
             kw.update(grid=(world, 1))
-    with native.Engine(p, obst, **kw) as e:
-        e.init_equilibrium()
-        e.run_steps(8, accelerate_first=True)
-        nset = _agree_max(settle_steps(e.last_run_seconds() / 8, e.steps_per_launch(), 0.2), dist_on)
-        e.run_steps(nset)
+    g = _RankGate("aux config4", dist_on)
+
+    def setup():
+        g.engine = native.Engine(p, obst, **kw)
+        g.engine.init_equilibrium()
+        g.engine.run_steps(8, accelerate_first=True)
+        return g.engine.last_run_seconds() / 8
+
+    per = g.run(setup)
+    g.gate("engine setup")
+    e = g.engine
+    try:
+        nset = _agree_max(settle_steps(per, e.steps_per_launch(), 0.2), dist_on)
+        g.run(lambda: e.run_steps(nset))
+        g.gate("settle steps")
         if dist_on:
             dist.barrier()
         t0 = time.perf_counter()
-        e.run_steps(steps)
-        if dist_on:
-            dist.barrier()
+        g.run(lambda: e.run_steps(steps))
+        g.gate("timed steps")   # the all_reduce doubles as the closing barrier
         secs = time.perf_counter() - t0
         kernel_used = e.kernel_in_use()
         spl = e.steps_per_launch()
         rect = e.local_rects()[0]
-        _, av = e.store(cells=False, n_av=steps)
+        av = g.run(lambda: e.store(cells=False, n_av=steps)[1])
+        g.gate("store")
+    finally:
+        e.close()
     finite = _agree_max(0 if np.isfinite(av).all() else 1, dist_on) == 0
     if dist_on:
         import torch
@@ -293,6 +310,33 @@ def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on
             # no rate for a run whose av_vels went non-finite (a broken lattice is not a measurement)
             "mlups": round(n * n * steps / secs / 1e6, 1) if finite else None,
             "ms_per_step": round(secs / steps * 1e3, 4)}
+
+
+class _RankGate:
+    """Host-side phases of a multi-rank aux measurement.  Each phase runs under
+    try/except on every rank; gate() then tells every rank, with one
+    all_reduce, whether all ranks finished the phase.  An exception on one rank
+    so ends the measurement on every rank at the same collective (and closes
+    the engine) instead of leaving the others blocked in the next collective
+    until the watchdog fires."""
+
+    def __init__(self, what: str, dist_on: bool):
+        self.what, self.dist_on, self.err, self.engine = what, dist_on, None, None
+
+    def run(self, fn):
+        if self.err is None:
+            try:
+                return fn()
+            except Exception as exc:  # recorded; gate() raises it on every rank
+                self.err = exc
+        return None
+
+    def gate(self, stage: str) -> None:
+        if _agree_max(1 if self.err is not None else 0, self.dist_on):
+            if self.engine is not None:
+                self.engine.close()
+            raise RuntimeError(f"{self.what}: {stage} failed on "
+                               + (f"this rank: {type(self.err).__name__}: {self.err}" if self.err else "another rank"))
 
 
 def _agree_max(v: int, dist_on: bool) -> int:
@@ -325,21 +369,33 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
         box = [native.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         kw.update(transport=native.TRANSPORT_RCCL, rank=rank, world=world, unique_id=box[0])
-    with native.Engine3D(p, obst, **kw) as e:
-        e.init_equilibrium()
-        e.run_steps(4)
-        nset = _agree_max(settle_steps(e.last_run_seconds() / 4, 2, 0.2), dist_on)
-        e.run_steps(nset)
+    g = _RankGate("aux config5 (D3Q19)", dist_on)
+
+    def setup():
+        g.engine = native.Engine3D(p, obst, **kw)
+        g.engine.init_equilibrium()
+        g.engine.run_steps(4)
+        return g.engine.last_run_seconds() / 4
+
+    per = g.run(setup)
+    g.gate("engine setup")
+    e = g.engine
+    try:
+        nset = _agree_max(settle_steps(per, 2, 0.2), dist_on)
+        g.run(lambda: e.run_steps(nset))
+        g.gate("settle steps")
         if dist_on:
             dist.barrier()
         t0 = time.perf_counter()
-        e.run_steps(steps)
-        if dist_on:
-            dist.barrier()
+        g.run(lambda: e.run_steps(steps))
+        g.gate("timed steps")   # the all_reduce doubles as the closing barrier
         secs = time.perf_counter() - t0
         dev = e.last_run_seconds()
         nzs = e.local_slabs()[0][1]
-        _, av = e.store(cells=False, n_av=steps)
+        av = g.run(lambda: e.store(cells=False, n_av=steps)[1])
+        g.gate("store")
+    finally:
+        e.close()
     finite = _agree_max(0 if np.isfinite(av).all() else 1, dist_on) == 0
     if dist_on:
         import torch
@@ -487,7 +543,8 @@ def check_failed_line(mrc: dict, n: int) -> dict:
             "multi_rank_bitwise": False, "multi_rank_check": mrc}
 
 
-# Device ms per fused launch of S steps at 8192^2 (profiles/r03/ab_spl_ow16.log,
+# Fallback only (calibrate_launch_ms measures these on the box at bench start):
+# device ms per fused launch of S steps at 8192^2 (profiles/r03/ab_spl_ow16.log,
 # 16-column aligned strips; tolerance S >= 7: the round-4 LP form with one row
 # per iteration, profiles/r04/ab_lp10.log): bitwise and tolerance collision; a
 # launch of 2..5 steps is bound by the lattice pass (~1.1 ms); a one-step
@@ -495,22 +552,89 @@ def check_failed_line(mrc: dict, n: int) -> dict:
 LAUNCH_MS = {"bitwise": {2: 1.12, 3: 1.07, 4: 1.10, 5: 1.18, 6: 1.39},
              "tolerance": {2: 1.11, 3: 1.07, 4: 1.08, 5: 1.10, 6: 1.10, 7: 1.21, 8: 1.33, 9: 1.50, 10: 1.55}}
 ONE_STEP_MS = 0.81
+_LAUNCH_CAL: dict = {}
+BOUND_FRAC = 0.75   # a roofline fraction at or above this names the bound
 
 
-def pick_spl(steps: int, requested: int, numerics: str = "bitwise", fused_remainder: bool = True) -> int:
+def _agree_max_f(v: float, dist_on: bool) -> float:
+    """The largest of every rank's float value."""
+    if not dist_on:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def calibrate_launch_ms(tnx: int, tny: int, numerics: str, local_rank: int, dist_on: bool, reps: int = 4) -> dict:
+    """Device ms per fused launch of S steps, for every S the collision allows
+    (bitwise 2..6, tolerance 2..10), and per one-step launch, measured on THIS
+    GPU at the bench tile with the library's own events (a single-domain
+    stream engine per S, placement probe included as in the timed engine),
+    max over ranks so every rank picks the same S.  Untimed, before the
+    warm-up; cached per tile and numerics.  Replaces reading LAUNCH_MS, which
+    a kernel change would silently invalidate (LAUNCH_MS stays the fallback
+    when a calibration engine cannot be built)."""
+    key = (tnx, tny, numerics)
+    if key in _LAUNCH_CAL:
+        return _LAUNCH_CAL[key]
+    smax = 10 if numerics == "tolerance" else 6
+    flags = native.FLAG_TOLERANCE if numerics == "tolerance" else 0
+    p = lio.Params(tnx, tny, 1, 10, 0.1, 0.005, 1.85)
+    obst = synthetic_obstacles(tnx, tny)
+    ms, one = {}, None
+    t0 = time.perf_counter()
+    try:
+        for i, S in enumerate(range(smax, 1, -1)):
+            with native.Engine(p, obst, devices=[local_rank], kernel=native.KERNEL_STREAM, flags=flags,
+                               steps_per_launch=S) as e:
+                e.init_equilibrium()
+                e.run_steps((60 if i == 0 else 2) * S, accelerate_first=True)   # clock ramp, then warm
+                e.run_steps(reps * S)
+                if e.run_stats() != (reps, 0):
+                    raise RuntimeError(f"S = {S}: launches {e.run_stats()}, expected ({reps}, 0)")
+                ms[S] = e.last_run_seconds() / reps * 1e3
+        # the one-step launch a K mod S = 1 remainder runs (vec4 at these widths)
+        with native.Engine(p, obst, devices=[local_rank], kernel=native.KERNEL_VEC4,
+                           flags=native.FLAG_ONE_STEP) as e:
+            e.init_equilibrium()
+            e.run_steps(2, accelerate_first=True)
+            e.run_steps(reps)
+            if e.run_stats() != (0, reps):
+                raise RuntimeError(f"one-step: launches {e.run_stats()}, expected (0, {reps})")
+            one = e.last_run_seconds() / reps * 1e3
+    except Exception as exc:  # recorded; the fallback table is used
+        log(f"launch calibration failed ({type(exc).__name__}: {exc}); using LAUNCH_MS")
+        ms, one = None, None
+    if _agree_max(1 if ms is None else 0, dist_on):   # any rank failed: every rank uses the fallback
+        res = {"source": "LAUNCH_MS fallback (profiles/r04)", "ms": dict(LAUNCH_MS[numerics]), "one_step_ms": ONE_STEP_MS}
+    else:
+        res = {"source": f"measured at bench start on this GPU ({tnx}x{tny}, {reps} launches per S, "
+                         f"{time.perf_counter() - t0:.1f} s)",
+               "ms": {S: round(_agree_max_f(v, dist_on), 4) for S, v in sorted(ms.items())},
+               "one_step_ms": round(_agree_max_f(one, dist_on), 4)}
+    _LAUNCH_CAL[key] = res
+    return res
+
+
+def pick_spl(steps: int, requested: int, numerics: str = "bitwise", fused_remainder: bool = True,
+             table: dict | None = None) -> int:
     """Steps per fused launch for a timed run of `steps` steps: the caller's
     choice if given, else the S whose launches finish `steps` soonest, counting
     the remainder steps % S as the library runs it (include/lbm_hip.h: one
-    fused launch when >= 2 steps, else one one-step launch) -- bitwise: the
-    driver's 20-step run is four 5-step launches, 1000 steps 166 six-step
-    launches + a 4-step one; tolerance: 2 x 10 and 100 x 10."""
+    fused launch when >= 2 steps, else one one-step launch).  `table`: a
+    calibrate_launch_ms result (else the LAUNCH_MS fallback) -- with it,
+    bitwise: the driver's 20-step run is four 5-step launches, 1000 steps 166
+    six-step launches + a 4-step one; tolerance: 2 x 10 and 100 x 10."""
     if requested:
         return requested
-    ms = LAUNCH_MS[numerics]
+    ms = {int(k): v for k, v in table["ms"].items()} if table else LAUNCH_MS[numerics]
+    one = table["one_step_ms"] if table else ONE_STEP_MS
 
     def est(S):
         r = steps % S
-        tail = ms[r] if (r >= 2 and fused_remainder) else r * ONE_STEP_MS
+        tail = ms[r] if (r >= 2 and fused_remainder) else r * one
         return (steps // S) * ms[S] + tail
 
     return min(sorted(ms, reverse=True), key=est) if steps > 0 else max(ms)
@@ -531,7 +655,12 @@ def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: 
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
     numerics = "tolerance" if kflags & native.FLAG_TOLERANCE else "bitwise"
-    spl = pick_spl(args.steps, args.spl, numerics) if kernel in (native.KERNEL_AUTO, native.KERNEL_STREAM) else args.spl
+    cal = None
+    if kernel in (native.KERNEL_AUTO, native.KERNEL_STREAM) and not args.spl:
+        cal = calibrate_launch_ms(tnx, tny, numerics, local_rank, dist_on) if args.calibrate else None
+        spl = pick_spl(args.steps, 0, numerics, table=cal)
+    else:
+        spl = args.spl
     eng = native.Engine(p, obst, parts=world, grid=(R, C),
                         transport=native.TRANSPORT_RCCL if dist_on else native.TRANSPORT_LOCAL,
                         rank=rank, world=world, devices=[local_rank], unique_id=uid, kernel=kernel, flags=kflags,
@@ -570,7 +699,7 @@ def measure_weak(tnx: int, tny: int, R: int, C: int, args, kernel: int, kflags: 
         _, av = eng.store(cells=False, n_av=args.steps)
         return {"nx": nx, "ny": ny, "elapsed": elapsed, "dev_secs": dev_secs, "finite": bool(np.all(np.isfinite(av))),
                 "kernel": eng.kernel_in_use(), "spl": eng.steps_per_launch(), "numerics": eng.numerics(),
-                "launches": eng.run_stats(),
+                "launches": eng.run_stats(), "calibration": cal,
                 "settle": {"steps": nset, "device_s": round(set_secs, 4),
                            "why": "GPU clock ramp over the first ~20-30 ms of back-to-back work "
                                   "(tools/settle_probe.py); untimed, same count on every rank"}}
@@ -684,6 +813,8 @@ def main() -> int:
                     help="value's collision: tolerance = LBM_FLAG_TOLERANCE (fp32, within the stated tolerance of "
                          "the reference: north_star's 'within a stated fp32 tolerance'); bitwise = every population "
                          "bit-identical to LastChance.cpp; the other mode is measured too (aux)")
+    ap.add_argument("--no-calibrate", dest="calibrate", action="store_false",
+                    help="pick S from the LAUNCH_MS fallback table instead of timing every S on this GPU first")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true")
     ap.add_argument("--no-d3q19", action="store_true")
@@ -748,9 +879,20 @@ def main() -> int:
     prof = load_traffic(wl_key)
     traffic = prof.get("hbm_bytes_per_launch")
     valu = prof.get("valu") or {}
-    # the bound that binds: the VALU pipe when the profile
-    # of this kernel shows it busy most of the time, else the lattice pass
-    bound = "valu" if valu.get("busy_frac", 0) >= 0.75 else "hbm"
+    # Which bound binds, from three fractions of one
+    # launch: the per-pass algorithmic bytes / launch time / HBM peak (frac),
+    # the PMC-counted HBM bytes / launch time / peak (what the channels really
+    # moved), and the VALU pipe's busy share of the SIMD cycles in quad-cycle
+    # units (4 x SQ_ACTIVE_INST_VALU / (SIMDs x GRBM_GUI_ACTIVE / 8),
+    # tools/pmc_traffic.py).  A bound is named only when its fraction reaches
+    # BOUND_FRAC; when none does, the launch is latency-bound (waits on loads,
+    # LDS and dependency chains), and it is called that.
+    frac_pass = achieved / HBM_PEAK_GBS
+    frac_counter = (traffic / per_launch_s / 1e9 / HBM_PEAK_GBS) if traffic else None
+    frac_valu = valu.get("busy_frac")
+    fracs = {"hbm": max(frac_pass, frac_counter or 0.0), "valu": frac_valu or 0.0}
+    top = max(fracs, key=fracs.get)
+    bound = top if fracs[top] >= BOUND_FRAC else "latency"
 
     out = {
         "metric": METRIC,
@@ -773,6 +915,10 @@ def main() -> int:
         "settle": m["settle"],
         "roofline": {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "frac_counter_bytes": round(frac_counter, 4) if frac_counter is not None else None,
+                     "frac_valu_issue": frac_valu,
+                     "bound_rule": (f"the largest of frac / frac_counter_bytes (HBM) and frac_valu_issue (VALU) "
+                                    f"if >= {BOUND_FRAC}, else 'latency'"),
                      "bytes_per_launch": BYTES_PER_UPDATE * cells_per_gpu,
                      "cell_updates_per_launch": steps_per_launch * cells_per_gpu,
                      "steps_per_launch": steps_per_launch,
@@ -786,7 +932,8 @@ def main() -> int:
         "av_vels_finite": m["finite"],
         "numerics": m["numerics"],
         "launches": {"fused": m["launches"][0], "one_step": m["launches"][1],
-                     "plan": launch_plan(args.steps, steps_per_launch, kernel_used == "stream")},
+                     "plan": launch_plan(args.steps, steps_per_launch, kernel_used == "stream"),
+                     "calibration": m["calibration"]},
     }
     if m["numerics"] == "tolerance":
         out["tolerance"] = TOLERANCE_NOTE

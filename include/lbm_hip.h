@@ -109,7 +109,9 @@ typedef struct lbm_config {
                                (single sub-domain without exchange); <0: off; 0: library default */
     int32_t flags;          /* LBM_FLAG_* */
     int32_t steps_per_launch; /* STREAM: time steps fused per launch (2..6; 2..10 with LBM_FLAG_TOLERANCE);
-                                 0 = library default (6; 10 with LBM_FLAG_TOLERANCE) */
+                                 0 = library default: 6 (10 with LBM_FLAG_TOLERANCE), lowered to the
+                                 deepest S every sub-domain allows (S cells, 2S across a decomposed
+                                 dimension) */
 } lbm_config;
 
 /* Route the periodic wrap of undecomposed dimensions through the transport
@@ -134,6 +136,12 @@ typedef struct lbm_config {
  * VEC4, the scalar resident tiles) stay bitwise.
  * lbm_numerics() reports which mode a handle runs. */
 #define LBM_FLAG_TOLERANCE 4
+/* Per-launch device timing (lbm_profile_summary): every launch is bracketed
+ * by a pair of HIP events on its own stream and folded per launch class after
+ * each run; hipGraph replay is off.  Costs a few microseconds per launch; off
+ * by default.  The counterpart of the reference's engine.printProfileSummary
+ * under LbmRunner -d (LbmRunner.cpp:115-122). */
+#define LBM_FLAG_PROFILE 8
 
 typedef struct lbm_handle lbm_handle;
 
@@ -291,6 +299,22 @@ int lbm_run_stats(lbm_handle *h, int32_t *fused_launches, int32_t *one_step_laun
  * (-1: no probe ran), how many pairs were timed, and (up to max_ms of) their
  * ms per launch. */
 int lbm_placement_probe(lbm_handle *h, int32_t *kept, int32_t *tried, float *ms_per_launch, int32_t max_ms);
+
+/* Launch-class device time accumulated over every run of a handle created
+ * with LBM_FLAG_PROFILE (since creation or lbm_profile_reset): one entry per
+ * class -- e.g. "stream_steps2d S=10 tolerance", "... interior" / "...
+ * boundary" on decomposed grids, "halo exchange WG (RCCL) + unpack",
+ * "accelerate_row", "finalize_av", "resident_steps (all steps, one launch)",
+ * the pipeline stages -- with its launch count and total / min / max ms
+ * between the events around each launch.  *n_out = number of classes; at most
+ * max_out entries are written.  LBM_E_STATE without the flag. */
+typedef struct lbm_kernel_time {
+    char name[64];
+    int64_t launches;
+    double total_ms, min_ms, max_ms;
+} lbm_kernel_time;
+int lbm_profile_summary(lbm_handle *h, lbm_kernel_time *out, int32_t max_out, int32_t *n_out);
+int lbm_profile_reset(lbm_handle *h);
 
 /* 0: every kernel of the handle is bitwise equal to the CPU oracle; 1: the
  * fused launches run the LBM_FLAG_TOLERANCE collision. */

@@ -67,7 +67,7 @@ hipError_t launch_pipe_rebound(const float *t, float *f, const uint8_t *obst, lo
 hipError_t launch_pipe_collision(const float *t, float *f, const uint8_t *obst, long long P, int pitch, int w, int h,
                                  float omega, float *partials, hipStream_t s);
 hipError_t launch_pipe_av(const float *partials, int n, float *av_local, int t, hipStream_t s);
-hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, hipStream_t s);
+hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, bool coop, hipStream_t s);
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s);
 hipError_t launch_debug_spin(int microseconds, hipStream_t s);
 }  // namespace lbm
@@ -250,6 +250,7 @@ struct lbm_handle {
     int res_per_cu = 1;      // LBM_RES_PER_CU: tiles per CU the choice may plan for (1 or 2)
     int res_early_poll = 0;  // LBM_RES_EARLY: v2 polls the ring after its first work item
     int res_version = 0;     // LBM_RES_V: 1 scalar 64-col tiles, 2 packed 128-col; 0 = by grid
+    bool res_coop = true;    // LBM_RES_COOP: cooperative launch of the resident kernel (else a plain one)
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
     float *res_partials = nullptr;
@@ -276,6 +277,88 @@ struct lbm_handle {
     // stall exposes the race and that the wait removes it.
     int delay_sub = -1, delay_us = 0;
     bool no_own_wait = false;
+    // LBM_FLAG_PROFILE: every launch bracketed by a pair of HIP events on its
+    // own stream, folded per launch class after each run (lbm_profile_summary;
+    // the counterpart of the reference's engine.printProfileSummary under -d,
+    // LbmRunner.cpp:115-122).  Off: no event is recorded.
+    bool profile = false;
+    struct ProfRec { int cls, dev; hipEvent_t a, b; };
+    struct ProfAcc { std::string name; long long launches = 0; double total_ms = 0, min_ms = 1e30, max_ms = 0; };
+    std::vector<ProfRec> prof_open;
+    std::vector<ProfAcc> prof_acc;
+    std::vector<std::pair<int, hipEvent_t>> prof_pool;  // (device, event) free list
+
+    int prof_class(const std::string &name) {
+        for (size_t i = 0; i < prof_acc.size(); ++i)
+            if (prof_acc[i].name == name) return (int)i;
+        prof_acc.push_back(ProfAcc{name});
+        return (int)prof_acc.size() - 1;
+    }
+    hipEvent_t prof_event(int dev) {
+        for (size_t i = 0; i < prof_pool.size(); ++i)
+            if (prof_pool[i].first == dev) {
+                hipEvent_t e = prof_pool[i].second;
+                prof_pool[i] = prof_pool.back();
+                prof_pool.pop_back();
+                return e;
+            }
+        hipEvent_t e = nullptr;
+        HIP_CHECK(hipEventCreate(&e));
+        return e;
+    }
+    // run `f` (which enqueues work on st of sub s) bracketed by profile events
+    template <class F>
+    void timed(const Sub &s, hipStream_t st, const std::string &cls, F &&f) {
+        if (!profile) {
+            f();
+            return;
+        }
+        ProfRec r{prof_class(cls), s.dev, prof_event(s.dev), prof_event(s.dev)};
+        HIP_CHECK(hipEventRecord(r.a, st));
+        f();
+        HIP_CHECK(hipEventRecord(r.b, st));
+        prof_open.push_back(r);
+    }
+    // after a run's streams are synchronised: fold this run's records
+    void prof_collect() {
+        for (auto &r : prof_open) {
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+            ProfAcc &a = prof_acc[r.cls];
+            a.launches++;
+            a.total_ms += ms;
+            a.min_ms = std::min(a.min_ms, (double)ms);
+            a.max_ms = std::max(a.max_ms, (double)ms);
+            prof_pool.push_back({r.dev, r.a});
+            prof_pool.push_back({r.dev, r.b});
+        }
+        prof_open.clear();
+    }
+    // records of a run that failed part-way are dropped (their events may never have been recorded)
+    void prof_drop() {
+        for (auto &r : prof_open) {
+            prof_pool.push_back({r.dev, r.a});
+            prof_pool.push_back({r.dev, r.b});
+        }
+        prof_open.clear();
+    }
+    void prof_release() {
+        for (auto &r : prof_open) {
+            prof_pool.push_back({r.dev, r.a});
+            prof_pool.push_back({r.dev, r.b});
+        }
+        prof_open.clear();
+        for (auto &e : prof_pool) (void)hipEventDestroy(e.second);
+        prof_pool.clear();
+    }
+    std::string part_name(bool fused_launch, bool interior, int steps) const {
+        const char *where = multi() ? (interior ? " interior" : " boundary") : "";
+        if (fused_launch && use_stream)
+            return std::string("stream_steps2d S=") + std::to_string(steps > 0 ? steps : spl) +
+                   (tolerance ? " tolerance" : "") + where;
+        if (fused_launch) return std::string("step2") + where;
+        return std::string(vec4 ? "step_vec4" : "step_scalar") + where;
+    }
     int run_fused = 0, run_single = 0;  // launches of the last run: fused (spl steps) / one-step
     // Tuning knobs (environment, read at create): LBM_TWO_STEP, LBM_MAX_BLOCKS,
     // LBM_LAYOUT (rows|planar), LBM_GRAPH_STEPS, LBM_FORCE_EXCHANGE.  Defaults
@@ -366,6 +449,7 @@ struct lbm_handle {
         if (const char *g = knob_str("LBM_STREAM_GUIDE")) set_guide(g);
         res_th_env = std::max(0, knob("LBM_RES_TH", 0));
         res_version = knob("LBM_RES_V", 0);
+        res_coop = knob("LBM_RES_COOP", res_coop ? 1 : 0) != 0;
         res_per_cu = std::min(std::max(knob("LBM_RES_PER_CU", res_per_cu), 1), 2);
         res_early_poll = knob("LBM_RES_EARLY", res_early_poll) != 0 ? 1 : 0;
         resident_max_cells = std::max(0, knob("LBM_RES_MAX_CELLS", (int)resident_max_cells));
@@ -888,6 +972,7 @@ struct lbm_handle {
         if (cfg.flags & LBM_FLAG_ONE_STEP) fused = false;
         force_exchange = (cfg.flags & LBM_FLAG_FORCE_EXCHANGE) != 0 || knob("LBM_FORCE_EXCHANGE", 0) != 0;
         tolerance = (cfg.flags & LBM_FLAG_TOLERANCE) != 0;
+        profile = (cfg.flags & LBM_FLAG_PROFILE) != 0;
         if (partition(p.nx, p.ny, parts, cfg.grid_rows, cfg.grid_cols, R, C, all_rects) != LBM_OK)
             throw lbm_failure(LBM_E_INVALID, "cannot partition " + std::to_string(p.nx) + "x" + std::to_string(p.ny) +
                                                  " into " + std::to_string(parts) + " parts");
@@ -923,8 +1008,16 @@ struct lbm_handle {
         if (tolerance) stream_cfg = tol_cfg == 3 ? 0 : tol_cfg;
         // the v3 kernel takes up to 6 steps per launch, 10 in the tolerance LP form
         const int s_max = tolerance ? 10 : 6;
-        const int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch
-                                               : std::min(tolerance ? tol_s : stream_s, s_max);
+        int S = cfg.steps_per_launch > 0 ? cfg.steps_per_launch : std::min(tolerance ? tol_s : stream_s, s_max);
+        if (cfg.steps_per_launch <= 0) {
+            // library default: the deepest S <= the default that every
+            // sub-domain allows (S cells, 2S across a decomposed dimension)
+            // instead of refusing small sub-domains an explicit request would fit
+            for (auto &r : all_rects) {
+                const int lw = (C > 1 || force_exchange) ? r.w / 2 : r.w, lh = (R > 1 || force_exchange) ? r.h / 2 : r.h;
+                S = std::min(S, std::max(2, std::min(lw, lh)));
+            }
+        }
         if (kernel == LBM_KERNEL_STREAM && (S < 2 || S > s_max))
             throw lbm_failure(LBM_E_INVALID, "steps_per_launch must be 2.." + std::to_string(s_max) +
                                                  (tolerance ? "" : " (up to 10 with LBM_FLAG_TOLERANCE)"));
@@ -1046,9 +1139,6 @@ struct lbm_handle {
         // (smallest tile height with one tile per CU first, except that 2-row
         // tiles are slower than 4-row ones on every grid measured:
         // profiles/r01/resident/)
-        // v5 (two-cell ring, one hand-off per two steps): whole 128 x 32 tiles only
-        if (res_version == 5 && p.nx % RES_TWV[RES5_32] == 0 && p.ny % RES_TH[RES5_32] == 0)
-            order.push_back(RES5_32);
         if (p.nx % 2 == 0 && (res_version == 0 || res_version == 2))
             order.insert(order.end(), {RES2_4, RES2_8, RES2_16, RES2_32, RES2_2, RES2_16x8});
         if (res_version == 0 || res_version == 1) order.insert(order.end(), {RES_4, RES_8, RES_16, RES_32, RES_64, RES_16x4});
@@ -1099,7 +1189,9 @@ struct lbm_handle {
         if (accelerate_first && s.accel_row >= 0) {
             const float w1 = p.density * p.accel / 9.f;
             const float w2 = p.density * p.accel / 36.f;
-            HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+            timed(s, s.s_comp, "accelerate_row", [&] {
+                HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+            });
         }
         if (steps > 0) {
             ResidentArgs a{};
@@ -1143,7 +1235,11 @@ struct lbm_handle {
                 HIP_CHECK(hipMemsetAsync(htrace, 0, n, s.s_comp));
                 a.htrace = htrace;
             }
-            HIP_CHECK(launch_resident(a, res_variant, tolerance && RES_VER[res_variant] >= 2, s.s_comp));
+            timed(s, s.s_comp, std::string("resident_steps (all steps, one launch)") + (tolerance && RES_VER[res_variant] >= 2 ? " tolerance" : ""),
+                  [&] {
+                      HIP_CHECK(launch_resident(a, res_variant, tolerance && RES_VER[res_variant] >= 2, res_coop,
+                                                s.s_comp));
+                  });
             if (htrace) {  // per tile and step: wait for the slowest neighbour, then the hop itself
                 std::vector<unsigned long long> hv((size_t)2 * trace_steps * ntiles);
                 HIP_CHECK(hipMemcpyAsync(hv.data(), htrace, hv.size() * 8, hipMemcpyDeviceToHost, s.s_comp));
@@ -1200,7 +1296,8 @@ struct lbm_handle {
                         ph[2] * us, ph[3] * us, ph[4] * us);
             }
             res_tag += (unsigned)steps;
-            HIP_CHECK(launch_resident_reduce(res_partials, s.av_local, steps, ntiles, s.s_comp));
+            timed(s, s.s_comp, "resident_reduce",
+                  [&] { HIP_CHECK(launch_resident_reduce(res_partials, s.av_local, steps, ntiles, s.s_comp)); });
             s.cur ^= 1;
         }
         HIP_CHECK(hipEventRecord(t1, s.s_comp));
@@ -1213,6 +1310,7 @@ struct lbm_handle {
             throw lbm_failure(LBM_E_INTERNAL, "resident kernel: a neighbour hand-off timed out (tiles not co-resident?)");
         last_seconds = ms * 1e-3;
         last_steps = steps;
+        prof_collect();
     }
 
     // Unfused pipeline, one kernel per stage (lbm_pipeline.hip): every step
@@ -1234,18 +1332,26 @@ struct lbm_handle {
             for (auto &s : subs) {
                 if (s.accel_row < 0 || p.ny < 2) continue;
                 set_device(s);
-                HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+                timed(s, s.s_comp, "accelerate_row", [&] {
+                    HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+                });
             }
             refresh_halos();
             for (auto &s : subs) {
                 set_device(s);
                 float *cells = s.o[s.cur], *tmp = s.o[1 - s.cur];
                 debug_delay(s, s.s_comp);
-                HIP_CHECK(launch_pipe_propagate(cells, tmp, s.plane, s.pitch, s.w, s.h, s.s_comp));
-                HIP_CHECK(launch_pipe_rebound(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, s.s_comp));
-                HIP_CHECK(launch_pipe_collision(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, p.omega,
-                                                s.pipe_partials, s.s_comp));
-                HIP_CHECK(launch_pipe_av(s.pipe_partials, pipe_blocks(s.w, s.h), s.av_local, t, s.s_comp));
+                timed(s, s.s_comp, "pipe_propagate",
+                      [&] { HIP_CHECK(launch_pipe_propagate(cells, tmp, s.plane, s.pitch, s.w, s.h, s.s_comp)); });
+                timed(s, s.s_comp, "pipe_rebound",
+                      [&] { HIP_CHECK(launch_pipe_rebound(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, s.s_comp)); });
+                timed(s, s.s_comp, "pipe_collision", [&] {
+                    HIP_CHECK(launch_pipe_collision(tmp, cells, s.obst, s.plane, s.pitch, s.w, s.h, p.omega,
+                                                    s.pipe_partials, s.s_comp));
+                });
+                timed(s, s.s_comp, "pipe_av", [&] {
+                    HIP_CHECK(launch_pipe_av(s.pipe_partials, pipe_blocks(s.w, s.h), s.av_local, t, s.s_comp));
+                });
             }
         }
         for (auto &s : subs) {
@@ -1261,6 +1367,7 @@ struct lbm_handle {
         last_seconds = ms * 1e-3;
         last_steps = steps;
         sync_all();
+        prof_collect();
     }
 
     void alloc_sub(Sub &s, const uint8_t *obstacles) {
@@ -1368,15 +1475,18 @@ struct lbm_handle {
             Sub &s = subs[0];
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_comm, s.ev_b, 0));
-            NCCL_CHECK(ncclGroupStart());
-            for (const lbm_xfer &x : exchange_posts(s.id, s.nb, s.remote, s.w, s.h, mode, hw)) {
-                if (x.op == LBM_XFER_SEND)
-                    NCCL_CHECK(ncclSend(s.send[x.dir], (size_t)x.floats, ncclFloat, x.peer, comm, s.s_comm));
-                else if (x.op == LBM_XFER_RECV)
-                    NCCL_CHECK(ncclRecv(s.recv[x.dir], (size_t)x.floats, ncclFloat, x.peer, comm, s.s_comm));
-            }
-            NCCL_CHECK(ncclGroupEnd());
-            HIP_CHECK(launch_halo_unpack(halo_args(s, target[0], mode, true), s.s_comm));
+            timed(s, s.s_comm, mode == HALO_WG ? "halo exchange WG (RCCL) + unpack" : "halo exchange W1 (RCCL) + unpack",
+                  [&] {
+                NCCL_CHECK(ncclGroupStart());
+                for (const lbm_xfer &x : exchange_posts(s.id, s.nb, s.remote, s.w, s.h, mode, hw)) {
+                    if (x.op == LBM_XFER_SEND)
+                        NCCL_CHECK(ncclSend(s.send[x.dir], (size_t)x.floats, ncclFloat, x.peer, comm, s.s_comm));
+                    else if (x.op == LBM_XFER_RECV)
+                        NCCL_CHECK(ncclRecv(s.recv[x.dir], (size_t)x.floats, ncclFloat, x.peer, comm, s.s_comm));
+                }
+                NCCL_CHECK(ncclGroupEnd());
+                HIP_CHECK(launch_halo_unpack(halo_args(s, target[0], mode, true), s.s_comm));
+            });
             HIP_CHECK(hipEventRecord(s.ev_u, s.s_comm));
             return;
         }
@@ -1391,17 +1501,24 @@ struct lbm_handle {
             if (!no_own_wait) HIP_CHECK(hipStreamWaitEvent(s.s_comm, s.ev_b, 0));
             for (int e = 0; e < 8; ++e) {
                 if (!s.remote[e]) continue;
-                Sub *src = local_sub(s.nb[e]);
+                const Sub *src = local_sub(s.nb[e]);
                 if (!src) throw lbm_failure(LBM_E_INTERNAL, "missing local neighbour");
                 HIP_CHECK(hipStreamWaitEvent(s.s_comm, src->ev_b, 0));
-                const size_t bytes = sizeof(float) * (size_t)msg_floats(mode, e, s.w, s.h, hw);
-                const float *from = src->send[OPP_DIR[e]];
-                if (src->dev == s.dev)
-                    HIP_CHECK(hipMemcpyAsync(s.recv[e], from, bytes, hipMemcpyDeviceToDevice, s.s_comm));
-                else
-                    HIP_CHECK(hipMemcpyPeerAsync(s.recv[e], s.dev, from, src->dev, bytes, s.s_comm));
             }
-            HIP_CHECK(launch_halo_unpack(halo_args(s, target[k], mode, true), s.s_comm));
+            timed(s, s.s_comm, mode == HALO_WG ? "halo exchange WG (device copies) + unpack"
+                                               : "halo exchange W1 (device copies) + unpack", [&] {
+                for (int e = 0; e < 8; ++e) {
+                    if (!s.remote[e]) continue;
+                    const Sub *src = local_sub(s.nb[e]);
+                    const size_t bytes = sizeof(float) * (size_t)msg_floats(mode, e, s.w, s.h, hw);
+                    const float *from = src->send[OPP_DIR[e]];
+                    if (src->dev == s.dev)
+                        HIP_CHECK(hipMemcpyAsync(s.recv[e], from, bytes, hipMemcpyDeviceToDevice, s.s_comm));
+                    else
+                        HIP_CHECK(hipMemcpyPeerAsync(s.recv[e], s.dev, from, src->dev, bytes, s.s_comm));
+                }
+                HIP_CHECK(launch_halo_unpack(halo_args(s, target[k], mode, true), s.s_comm));
+            });
             HIP_CHECK(hipEventRecord(s.ev_u, s.s_comm));
         }
     }
@@ -1568,7 +1685,8 @@ struct lbm_handle {
         for (size_t k = 0; k < subs.size(); ++k) {
             Sub &s = subs[k];
             set_device(s);
-            HIP_CHECK(launch_halo_pack(halo_args(s, s.o[s.cur], mode, false), s.s_comp));
+            timed(s, s.s_comp, "halo_pack",
+                  [&] { HIP_CHECK(launch_halo_pack(halo_args(s, s.o[s.cur], mode, false), s.s_comp)); });
             HIP_CHECK(hipEventRecord(s.ev_b, s.s_comp));
             tgt[k] = s.o[s.cur];
         }
@@ -1626,7 +1744,8 @@ struct lbm_handle {
     void launch_once(bool two, int steps = 0) {
         if (!multi()) {
             Sub &s = subs[0];
-            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp, steps));
+            timed(s, s.s_comp, part_name(two, true, steps),
+                  [&] { HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp, steps)); });
             s.cur ^= 1;
             return;
         }
@@ -1644,7 +1763,8 @@ struct lbm_handle {
             HIP_CHECK(hipStreamWaitEvent(s.s_bnd, s.ev_i, 0));
             wait_exchange_on(s, s.s_bnd);
             debug_delay(s, s.s_bnd);
-            HIP_CHECK(launch_part(s, s.cur, two, false, s.s_bnd, steps));
+            timed(s, s.s_bnd, part_name(two, false, steps),
+                  [&] { HIP_CHECK(launch_part(s, s.cur, two, false, s.s_bnd, steps)); });
             HIP_CHECK(hipEventRecord(s.ev_b, s.s_bnd));
             HIP_CHECK(hipEventRecord(s.ev_bp[s.cur], s.s_bnd));
             tgt[k] = s.o[1 - s.cur];
@@ -1654,7 +1774,8 @@ struct lbm_handle {
             set_device(s);
             HIP_CHECK(hipStreamWaitEvent(s.s_comp, s.ev_bp[1 - s.cur], 0));  // B(t-1)
             debug_delay(s, s.s_comp);
-            HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp, steps));
+            timed(s, s.s_comp, part_name(two, true, steps),
+                  [&] { HIP_CHECK(launch_part(s, s.cur, two, true, s.s_comp, steps)); });
             HIP_CHECK(hipEventRecord(s.ev_i, s.s_comp));
         }
         for (auto &s : subs) s.cur ^= 1;
@@ -1715,6 +1836,7 @@ struct lbm_handle {
         if (steps < 0) throw lbm_failure(LBM_E_INVALID, "steps must be >= 0");
         ensure_av(std::max(steps, 1));
         run_fused = run_single = 0;
+        prof_drop();
         if (resident) {
             run_resident(steps, accelerate_first);
             run_fused = steps > 0 ? 1 : 0;
@@ -1733,7 +1855,7 @@ struct lbm_handle {
         const int per_launch = fused ? spl : 1;
         const int launches = steps / per_launch;
         const int chunk = 2 * graph_steps;  // launches per graph replay (even: parity unchanged)
-        const bool use_graph = !multi() && graph_steps > 0 && launches >= chunk;
+        const bool use_graph = !multi() && !profile && graph_steps > 0 && launches >= chunk;
         if (use_graph) (void)graph_for(subs[0].cur);  // capture + instantiate outside the timed region
         Sub &s0 = subs[0];
         set_device(s0);
@@ -1756,7 +1878,9 @@ struct lbm_handle {
             for (auto &s : subs) {
                 if (s.accel_row < 0) continue;
                 set_device(s);
-                HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+                timed(s, s.s_comp, "accelerate_row", [&] {
+                    HIP_CHECK(launch_accelerate(s.o[s.cur], s.obst, s.plane, s.pitch, s.w, s.accel_row, w1, w2, s.s_comp));
+                });
             }
             refresh_halos();
         }
@@ -1786,7 +1910,8 @@ struct lbm_handle {
         if (rem > 0) ring_stale = true;                    // ... the next run restores the WG ring first
         for (auto &s : subs) {
             set_device(s);
-            HIP_CHECK(launch_finalize(s.partials[1 - s.cur], s.av_local, s.ctl, s.s_comp));
+            timed(s, s.s_comp, "finalize_av",
+                  [&] { HIP_CHECK(launch_finalize(s.partials[1 - s.cur], s.av_local, s.ctl, s.s_comp)); });
             HIP_CHECK(hipEventRecord(s.ev_end, s.s_comp));
         }
         set_device(s0);
@@ -1798,6 +1923,7 @@ struct lbm_handle {
         last_seconds = ms * 1e-3;
         last_steps = steps;
         sync_all();
+        prof_collect();
         dump_trace();
     }
 
@@ -1952,6 +2078,7 @@ struct lbm_handle {
 
     void destroy() {
         drop_graphs();
+        prof_release();
         for (auto &s : subs) {
             if (hipSetDevice(s.dev) != hipSuccess) continue;
             (void)hipDeviceSynchronize();
@@ -2189,6 +2316,32 @@ int lbm_run_stats(lbm_handle *h, int32_t *fused_launches, int32_t *one_step_laun
     if (!h) return LBM_E_INVALID;
     if (fused_launches) *fused_launches = h->run_fused;
     if (one_step_launches) *one_step_launches = h->run_single;
+    return LBM_OK;
+}
+
+int lbm_profile_summary(lbm_handle *h, lbm_kernel_time *out, int32_t max_out, int32_t *n_out) {
+    if (!h || !n_out) return LBM_E_INVALID;
+    if (!h->profile) {
+        h->err = "handle was not created with LBM_FLAG_PROFILE";
+        return LBM_E_STATE;
+    }
+    *n_out = (int32_t)h->prof_acc.size();
+    for (int i = 0; out && i < (int)h->prof_acc.size() && i < max_out; ++i) {
+        const auto &a = h->prof_acc[i];
+        lbm_kernel_time &k = out[i];
+        memset(&k, 0, sizeof(k));
+        snprintf(k.name, sizeof(k.name), "%s", a.name.c_str());
+        k.launches = a.launches;
+        k.total_ms = a.total_ms;
+        k.min_ms = a.launches ? a.min_ms : 0.0;
+        k.max_ms = a.max_ms;
+    }
+    return LBM_OK;
+}
+
+int lbm_profile_reset(lbm_handle *h) {
+    if (!h) return LBM_E_INVALID;
+    h->prof_acc.clear();
     return LBM_OK;
 }
 

@@ -189,16 +189,17 @@ constexpr int RES2_TW = 128;
 enum ResVariant : int {
     RES_64 = 0, RES_32 = 1, RES_16 = 2, RES_16x4 = 3, RES_8 = 4, RES_4 = 5,           // v1
     RES2_32 = 6, RES2_16 = 7, RES2_8 = 8, RES2_4 = 9, RES2_2 = 10,                    // v2
-    RES2_16x8 = 11,                                                                     // v2, 8 waves: 2 tiles per CU
-    RES5_32 = 12                                                                        // v5: two-cell ring (lbm_resident2.hip)
+    RES2_16x8 = 11                                                                      // v2, 8 waves: 2 tiles per CU
 };
-constexpr int NUM_RES = 13;
-constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 16, 32};
-constexpr int RES_TWV[NUM_RES] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128, 128, 128};
-constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 5};
-// granule values per (tile, direction, position): v1/v2 three planes; v5 the
-// nine values of a two-deep band (lbm_resident2.hip)
-constexpr int RES_GV[NUM_RES] = {3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 9};
+// (v5, a two-cell ring with one hand-off per two steps, lost its A/B to v2 in
+// round 4 -- 4.4 vs 4.0 us per step, DESIGN.md section 4.4,
+// profiles/r04/res5/ -- and was removed from the sources in round 5.)
+constexpr int NUM_RES = 12;
+constexpr int RES_TH[NUM_RES] = {64, 32, 16, 16, 8, 4, 32, 16, 8, 4, 2, 16};
+constexpr int RES_TWV[NUM_RES] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128, 128};
+constexpr int RES_VER[NUM_RES] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2};
+// granule values per (tile, direction, position): three planes
+constexpr int RES_GV[NUM_RES] = {3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3};
 constexpr int RES_GW = 128;  // granule positions per (tile, direction, plane), both versions
 
 struct ResidentArgs {

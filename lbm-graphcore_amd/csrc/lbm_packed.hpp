@@ -18,17 +18,12 @@
 //     holding a smaller density takes the compiler's IEEE division instead
 //     (a wave-uniform branch, never taken in physical states).
 // |u| = sqrt(u^2) feeds only av_vels and uses v_sqrt_f32 (sqrt_av below).
-// LBM_EXP_FASTDIV (A/B builds only, tools/build_variant.sh; default 0): the
-// shared-reciprocal n / rho -- 1 unguarded (+10 % at 8192^2, not exact for
-// every input), 2 guarded (exact, no faster): DESIGN.md section 9,
-// profiles/r04/fastdiv/.
+// (The shared-reciprocal n / rho was measured as library variants in round 4:
+// +10 % unguarded but not exact for every input, no gain guarded -- DESIGN.md
+// section 9, profiles/r04/fastdiv/; removed from the sources in round 5.)
 #pragma once
 
 #include "lbm_device.hpp"
-
-#ifndef LBM_EXP_FASTDIV
-#define LBM_EXP_FASTDIV 0
-#endif
 
 namespace lbm {
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -134,37 +129,8 @@ __device__ __forceinline__ f2 collide2(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bo
 __device__ __forceinline__ f2 collide2u(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, bool accrow,
                                         float omega, float omo, float w1, float w2) {
     const f2 rho = s[0] + s[1] + s[2] + s[3] + s[4] + s[5] + s[6] + s[7] + s[8];
-#if LBM_EXP_FASTDIV
-    // EXPERIMENT (tools/build_variant.sh, timing only): the shared-reciprocal
-    // division y = rcp(rho) + one Newton step, q = n*y, q' = fma(n - rho*q, y, q);
-    // 2: with the wave-uniform range guard a bitwise form would need
-    const f2 nux = s[1] + s[5] + s[8] - (s[3] + s[6] + s[7]);
-    const f2 nuy = s[2] + s[5] + s[6] - (s[4] + s[7] + s[8]);
-    f2 ux, uy;
-    bool fast = true;
-    if (LBM_EXP_FASTDIV == 2) {
-        auto ok = [](float r, float a, float b) {
-            const unsigned ur = __float_as_uint(r) - 0x21800000u, ua = (__float_as_uint(a) & 0x7fffffffu) - 0x21800000u,
-                           ub = (__float_as_uint(b) & 0x7fffffffu) - 0x21800000u;
-            return ur < 0x3c000000u && (ua < 0x3c000000u || __float_as_uint(a) == 0u) &&
-                   (ub < 0x3c000000u || __float_as_uint(b) == 0u);
-        };
-        fast = __builtin_amdgcn_ballot_w64(!(ok(rho.x, nux.x, nuy.x) && ok(rho.y, nux.y, nuy.y))) == 0;
-    }
-    if (fast) {
-        const f2 y0 = f2{__builtin_amdgcn_rcpf(rho.x), __builtin_amdgcn_rcpf(rho.y)};
-        const f2 y = fma2(fma2(-rho, y0, mk2(1.f)), y0, y0);
-        const f2 qx = nux * y, qy = nuy * y;
-        ux = fma2(fma2(-rho, qx, nux), y, qx);
-        uy = fma2(fma2(-rho, qy, nuy), y, qy);
-    } else {
-        ux = nux / rho;
-        uy = nuy / rho;
-    }
-#else
     const f2 ux = (s[1] + s[5] + s[8] - (s[3] + s[6] + s[7])) / rho;
     const f2 uy = (s[2] + s[5] + s[6] - (s[4] + s[7] + s[8])) / rho;
-#endif
     const f2 usq = ux * ux + uy * uy;
     const f2 csq = mk2(1.00f) - usq * mk2(1.50f);
     const f2 ld1 = div_const<9>(rho) * mk2(omega);

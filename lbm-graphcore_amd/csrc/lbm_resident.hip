@@ -607,8 +607,6 @@ __global__ __launch_bounds__(256) void resident_reduce(const float *partials, fl
 
 // ---- host side ---------------------------------------------------------------
 
-const void *resident_kernel_r2(bool tol, int &threads);  // lbm_resident2.hip
-
 namespace {
 template <int NW, int R>
 const void *resident_fn() {
@@ -626,7 +624,6 @@ const void *resident_fn2(bool tol) {
 // scalar v1 tiles have only the bitwise one
 const void *resident_kernel(int variant, int &threads, bool tol) {
     switch (variant) {
-        case RES5_32: return resident_kernel_r2(tol, threads);  // lbm_resident2.hip
         case RES_64: threads = 1024; return resident_fn<16, 4>();
         case RES_32: threads = 1024; return resident_fn<16, 2>();
         case RES_16: threads = 1024; return resident_fn<16, 1>();
@@ -656,13 +653,19 @@ hipError_t resident_capacity(int variant, int device, bool tol, int &capacity) {
     return hipSuccess;
 }
 
-hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, hipStream_t s) {
+// coop: hipLaunchCooperativeKernel (the runtime rejects a grid that cannot be
+// fully resident; HIP runs it on its own cooperative queue); else a plain
+// launch of a grid the engine has already sized to the occupancy capacity
+// (resident_capacity), co-resident on an otherwise idle device -- and if it
+// ever is not, the kernel's 2 s poll deadline drains the grid and the run
+// reports LBM_E_INTERNAL instead of hanging.
+hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, bool coop, hipStream_t s) {
     int threads = 0;
     const void *fn = resident_kernel(variant, threads, tol);
     ResidentArgs arg = a;
     void *params[] = {&arg};
-    // cooperative: the runtime rejects a grid that cannot be fully resident
-    return hipLaunchCooperativeKernel(fn, dim3(a.tiles_x * a.tiles_y), dim3(threads), params, 0, s);
+    if (coop) return hipLaunchCooperativeKernel(fn, dim3(a.tiles_x * a.tiles_y), dim3(threads), params, 0, s);
+    return hipLaunchKernel(fn, dim3(a.tiles_x * a.tiles_y), dim3(threads), params, 0, s);
 }
 
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s) {

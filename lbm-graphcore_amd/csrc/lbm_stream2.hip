@@ -217,6 +217,12 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         // vs 254)
         const bool cold = GUARD && j < g.j0 + 2 * L;
         if (!LP && cold) continue;
+        // LP: this level's running |u| sum is read from LDS here, before the
+        // collision, and added to after it: read right before its use (as the
+        // plain `lps[] +=` compiles), its lgkmcnt(0) wait stalled the wave
+        // once per level for a full LDS round trip
+        float usum = 0.f;
+        if constexpr (LP) usum = lps[b * 64];
 
         f2 o[Q];
         const bool oa = OBST && ((st.oba >> L) & 1u), ob = OBST && ((st.obb >> L) & 1u);
@@ -257,8 +263,9 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
             const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
             const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
             if constexpr (LP)
-                lps[b * 64] += ua + ub;  // LP: the per-level |u| sums in LDS, not VGPRs (as an LDS
-                                         // float atomic add with no return: 1.6x slower, profiles/r04/ab_libs.log)
+                lps[b * 64] = usum + (ua + ub);  // LP: the per-level |u| sums in LDS, not VGPRs (as an LDS
+                                                 // float atomic add with no return: 1.6x slower,
+                                                 // profiles/r04/ab_libs.log)
             else
                 st.tot[b] += ua + ub;
         }

@@ -25,7 +25,7 @@ LBM_OK = 0
 LBM_E_INVALID, LBM_E_HIP, LBM_E_RCCL, LBM_E_NOMEM, LBM_E_STATE, LBM_E_INTERNAL = -1, -2, -3, -4, -5, -6
 TRANSPORT_LOCAL, TRANSPORT_RCCL = 0, 1
 KERNEL_AUTO, KERNEL_SCALAR, KERNEL_VEC4, KERNEL_STEP2, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PIPELINE = range(7)
-FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP, FLAG_TOLERANCE = 1, 2, 4
+FLAG_FORCE_EXCHANGE, FLAG_ONE_STEP, FLAG_TOLERANCE, FLAG_PROFILE = 1, 2, 4, 8
 XFER_SEND, XFER_RECV, XFER_SELF = 0, 1, 2
 HALO_W1, HALO_WG = 1, 2
 
@@ -37,7 +37,7 @@ EXPORTED = [
     "lbm_run", "lbm_run_steps", "lbm_store", "lbm_load_cells_local", "lbm_store_local", "lbm_local_cells",
     "lbm_last_run_seconds",
     "lbm_total_free_cells", "lbm_local_rects", "lbm_kernel_in_use", "lbm_steps_per_launch",
-    "lbm_run_stats", "lbm_placement_probe", "lbm_numerics", "lbm_nonfinite_count", "lbm_source_hash",
+    "lbm_run_stats", "lbm_profile_summary", "lbm_profile_reset", "lbm_placement_probe", "lbm_numerics", "lbm_nonfinite_count", "lbm_source_hash",
     "lbm_last_error", "lbm_destroy",
 ]
 # every symbol include/lbm3d_hip.h declares (D3Q19 extension)
@@ -94,6 +94,12 @@ class Params3D(ctypes.Structure):
 
 class Rect(ctypes.Structure):
     _fields_ = [("x0", ctypes.c_int32), ("y0", ctypes.c_int32), ("w", ctypes.c_int32), ("h", ctypes.c_int32)]
+
+
+class KernelTime(ctypes.Structure):
+    """lbm_kernel_time (include/lbm_hip.h)."""
+    _fields_ = [("name", ctypes.c_char * 64), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double),
+                ("min_ms", ctypes.c_double), ("max_ms", ctypes.c_double)]
 
 
 class Xfer(ctypes.Structure):
@@ -156,6 +162,8 @@ def load_library() -> ctypes.CDLL:
         "lbm_kernel_in_use": ([H], i32),
         "lbm_steps_per_launch": ([H], i32),
         "lbm_run_stats": ([H, i32p, i32p], ctypes.c_int),
+        "lbm_profile_summary": ([H, ctypes.POINTER(KernelTime), i32, i32p], ctypes.c_int),
+        "lbm_profile_reset": ([H], ctypes.c_int),
         "lbm_placement_probe": ([H, i32p, i32p, f32p, i32], ctypes.c_int),
         "lbm_numerics": ([H], i32),
         "lbm_nonfinite_count": ([H, ctypes.POINTER(i64)], ctypes.c_int),
@@ -366,6 +374,18 @@ class Engine:
         a, b = ctypes.c_int32(), ctypes.c_int32()
         self._check(self._L.lbm_run_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def profile_summary(self):
+        """[{name, launches, total_ms, min_ms, max_ms}] per launch class (LBM_FLAG_PROFILE handles)."""
+        n = ctypes.c_int32()
+        self._check(self._L.lbm_profile_summary(self._h, None, 0, ctypes.byref(n)))
+        buf = (KernelTime * max(n.value, 1))()
+        self._check(self._L.lbm_profile_summary(self._h, buf, n.value, ctypes.byref(n)))
+        return [{"name": k.name.decode(), "launches": k.launches, "total_ms": k.total_ms, "min_ms": k.min_ms,
+                 "max_ms": k.max_ms} for k in buf[:n.value]]
+
+    def profile_reset(self) -> None:
+        self._check(self._L.lbm_profile_reset(self._h))
 
     def placement(self):
         """(kept pair or -1, [ms per launch of each pair tried]) of the placement probe."""

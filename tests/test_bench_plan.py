@@ -32,3 +32,15 @@ def test_launch_plan_strings():
     assert bench.launch_plan(13, 6, True) == "2 x 6 + 1 x 1"
     assert bench.launch_plan(20, 5, True) == "4 x 5"
     assert bench.launch_plan(7, 2, False) == "3 x 2 + 1 x 1"
+
+
+def test_pick_spl_follows_a_calibration_table():
+    """With a measured table (calibrate_launch_ms) the choice follows the box,
+    not the LAUNCH_MS fallback."""
+    flat = {"ms": {S: 1.0 for S in range(2, 11)}, "one_step_ms": 0.8}
+    assert bench.pick_spl(20, 0, "tolerance", table=flat) == 10          # fewest launches
+    slow10 = {"ms": {**{S: 1.0 for S in range(2, 10)}, 10: 9.0}, "one_step_ms": 0.8}
+    assert bench.pick_spl(20, 0, "tolerance", table=slow10) == 9          # 2 x 9 + a 2-step launch: 3 ms
+    assert bench.pick_spl(18, 0, "tolerance", table=slow10) == 9          # 2 x 9
+    json_keys = {"ms": {**{str(S): 1.0 for S in range(2, 6)}, "6": 1.4}, "one_step_ms": 0.8}   # keys after a JSON trip
+    assert bench.pick_spl(20, 0, "bitwise", table=json_keys) == 5

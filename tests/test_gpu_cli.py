@@ -54,6 +54,42 @@ def test_lbm_runner_128(gpu_lib, tmp_path, args):
     assert re_out == pytest.approx(m["reynolds_last_av"], rel=2e-3 if "--tolerance" in args else 2e-4)
     res = _gate(tmp_path, "128x128")
     assert res["passed"], res
+    # -d: the per-launch-class device-time summary (LbmRunner.cpp:115-122's profile summary)
+    assert "Profile summary" in r.stdout
+    if "step kernel: resident" in r.stdout:   # AUTO keeps 128x128 resident on chip
+        assert "resident_steps" in r.stdout and "HBM roofline: n/a" in r.stdout
+    else:
+        assert re.search(r"% of the 8000 GB/s HBM roofline", r.stdout)
+
+
+def test_lbm_runner_json_record_and_profile(gpu_lib, tmp_path):
+    """--json appends one record whose rates agree with the printed ones and
+    whose profile classes account for the fused launches of every run."""
+    exe = PKG / "build" / "lbm_runner"
+    out = tmp_path / "runs.jsonl"
+    for _ in range(2):
+        r = subprocess.run([str(exe), "--params", str(GOLD / "params" / "input_128x256.params"),
+                            "--obstacles", str(GOLD / "params" / "obstacles_128x256.dat"), "--runs", "2",
+                            "--out-dir", str(tmp_path), "--kernel", "stream", "--spl", "5", "-d", "--json", str(out)],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+    recs = [json.loads(line) for line in out.read_text().splitlines()]
+    assert len(recs) == 2
+    rec = recs[-1]
+    p, _ = load_problem("128x256")
+    assert rec["kernel"] == "stream" and rec["steps_per_launch"] == 5 and rec["numerics"] == "bitwise"
+    assert rec["steps"] == p.max_iters and rec["hbm_passes_per_run"] == p.max_iters // 5 + (p.max_iters % 5 > 1) + \
+        (p.max_iters % 5 == 1)
+    printed = float(re.search(r"MLUPS: (\S+)", r.stdout).group(1))
+    assert rec["mlups"] == pytest.approx(printed, rel=1e-3)
+    assert rec["gbs_per_pass"] == pytest.approx(72 * p.nx * p.ny * rec["hbm_passes_per_run"] / rec["avg_seconds"] / 1e9,
+                                                rel=1e-4)
+    assert 0 < rec["hbm_roofline_frac"] < 1
+    prof = {k["name"]: k for k in rec["profile"]}
+    fused = prof["stream_steps2d S=5"]
+    assert fused["launches"] == 3 * (p.max_iters // 5)   # three runs: lbm_run + 2 timed
+    assert 0 < fused["min_ms"] <= fused["total_ms"] / fused["launches"] <= fused["max_ms"]
+    assert prof["accelerate_row"]["launches"] == 3 and prof["finalize_av"]["launches"] == 3
 
 
 def test_compare_lbm_128x256(gpu_lib, tmp_path):

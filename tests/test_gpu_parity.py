@@ -434,6 +434,24 @@ def test_stream_size_limits(gpu_lib):
         assert e.kernel_in_use() == "resident"
     with gpu_lib.Engine(p, obst, parts=2, devices=[0]) as e:
         assert e.kernel_in_use() in ("step2", "stream")
+    # steps_per_launch = 0 (library default): the deepest S the sub-domains
+    # allow, instead of refusing them (the tolerance default 10 needs 20 cells
+    # across a decomposed dimension; 2 x 17-column halves take S = 8)
+    p2, obst2 = load_problem("128x256", iters=16)
+    p2 = lio.Params(34, 40, 16, p2.reynolds_dim, p2.density, p2.accel, p2.omega)
+    obst2 = np.zeros((40, 34), np.uint8)
+    obst2[0, :] = 1
+    cells0 = lio.init_cells(p2)
+    ref, _ = oracle.run(p2, obst2, 16, cells0)
+    for flags, want in ((gpu_lib.FLAG_TOLERANCE, 8), (0, 6)):
+        with gpu_lib.Engine(p2, obst2, parts=2, grid=(1, 2), devices=[0], kernel=gpu_lib.KERNEL_STREAM,
+                            flags=flags, steps_per_launch=0) as e:
+            assert e.kernel_in_use() == "stream" and e.steps_per_launch() == want
+            e.load_cells(cells0)
+            e.run_steps(16, accelerate_first=True)
+            cells, _ = e.store(n_av=16)
+        if not flags:
+            assert np.array_equal(cells, ref)
 
 
 @pytest.mark.parametrize("mode", ["step2", "stream2", "stream3", "stream4", "stream5", "stream6", "plain6"])
@@ -508,48 +526,6 @@ def test_resident_1024_runs_continue(gpu_lib, ver, monkeypatch):
     ref, ref_av = oracle.run(p, obst, 6, ref, accelerate_first=False)
     assert np.array_equal(cells, ref)
     np.testing.assert_allclose(av, ref_av, rtol=1e-4)
-
-
-@pytest.mark.parametrize("nx,ny,steps", [(128, 32, 9), (256, 96, 1), (256, 96, 2), (256, 96, 37), (384, 64, 8)])
-def test_resident_ring2_bitwise(gpu_lib, nx, ny, steps, monkeypatch):
-    """v5 (lbm_resident2.hip: two-cell ghost ring, one hand-off per two steps)
-    on whole 128 x 32 tilings -- one tile (its own neighbour in all eight
-    directions), 2 x 3 and 3 x 2 tiles; odd step counts end on a ring step
-    without a hand-off: lattice bitwise == oracle."""
-    monkeypatch.setenv("LBM_RES_V", "5")
-    p = lio.Params(nx, ny, steps, 10, 0.1, 0.02, 1.7)
-    obst = np.zeros((ny, nx), np.uint8)
-    obst[0, :] = obst[-1, :] = 1
-    obst[ny // 3:, nx // 3] = 1
-    obst[5:9, 127:131] = 1  # across a tile corner (and the wrap on one tile)
-    rng = np.random.default_rng(nx * 1000 + ny + steps)
-    cells0 = (lio.init_cells(p) * (1 + 0.05 * rng.standard_normal((ny, nx, 9)))).astype(np.float32)
-    ref, ref_av = oracle.run(p, obst, steps, cells0)
-    with gpu_lib.Engine(p, obst, kernel=gpu_lib.KERNEL_RESIDENT) as e:
-        assert e.kernel_in_use() == "resident"  # LBM_RES_V=5 offers v5 alone: built, or the engine raises
-        e.load_cells(cells0)
-        e.run_steps(steps, accelerate_first=True)
-        cells, av = e.store(n_av=steps)
-    assert np.array_equal(cells, ref)
-    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
-
-
-def test_resident_ring2_1024_full_run(gpu_lib, monkeypatch):
-    """v5 on the BASELINE config-2 grid (1024^2, 20 000 steps): the final
-    lattice's sha256 == the oracle manifest's; av_vels ~ oracle; runs of odd
-    lengths continue one state (granule tags keep counting across runs)."""
-    monkeypatch.setenv("LBM_RES_V", "5")
-    p, obst = load_problem("1024x1024")
-    m = oracle_manifest("1024x1024")
-    with gpu_lib.Engine(p, obst, kernel=gpu_lib.KERNEL_RESIDENT) as e:
-        assert e.kernel_in_use() == "resident"
-        e.load_cells(lio.init_cells(p))
-        e.run_steps(3, accelerate_first=True)
-        e.run_steps(1)
-        e.run_steps(p.max_iters - 4)
-        cells, av = e.store(n_av=p.max_iters - 4)
-    assert sha(cells) == m["final_f_sha256"]
-    np.testing.assert_allclose(av, oracle_av_vels("1024x1024")[4:], rtol=AV_RTOL)
 
 
 def test_resident_rejects_decomposition(gpu_lib):

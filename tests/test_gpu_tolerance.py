@@ -209,29 +209,6 @@ def test_tolerance_resident_tiles_vs_stream(gpu_lib, th, monkeypatch):
     np.testing.assert_allclose(a[1], b[1], rtol=1e-5)
 
 
-@pytest.mark.parametrize("steps", [16, 18])
-def test_tolerance_resident_ring2_vs_stream(gpu_lib, steps, monkeypatch):
-    """v5 (two-cell ring) with the tolerance collision: the same lattice bit
-    for bit as the stream kernel (6-step launches, a fused 4-step remainder at 16)."""
-    monkeypatch.setenv("LBM_RES_V", "5")
-    rng = np.random.default_rng(steps)
-    p = lio.Params(256, 96, steps, 10, 0.1, 0.02, 1.7)
-    obst = (rng.random((96, 256)) < 0.03).astype(np.uint8)
-    obst[0, :] = 1
-    cells0 = (lio.init_cells(p) * (1 + 0.04 * rng.standard_normal((96, 256, 9)))).astype(np.float32)
-    out = {}
-    for kernel in (gpu_lib.KERNEL_RESIDENT, gpu_lib.KERNEL_STREAM):
-        with gpu_lib.Engine(p, obst, kernel=kernel, flags=gpu_lib.FLAG_TOLERANCE, steps_per_launch=6) as e:
-            assert e.numerics() == "tolerance" and e.kernel_in_use() == ("resident" if kernel == gpu_lib.KERNEL_RESIDENT
-                                                                         else "stream")
-            e.load_cells(cells0)
-            e.run_steps(steps, accelerate_first=True)
-            out[kernel] = e.store(n_av=steps)
-    a, b = out[gpu_lib.KERNEL_RESIDENT], out[gpu_lib.KERNEL_STREAM]
-    assert np.array_equal(a[0], b[0])
-    np.testing.assert_allclose(a[1], b[1], rtol=1e-5)
-
-
 @pytest.mark.parametrize("steps", [24, 30])
 def test_tolerance_steps_per_launch_invariant(gpu_lib, steps):
     """Tolerance launches of S = 2..10 steps (plain forms up to 6, the LP form

@@ -64,3 +64,16 @@ def test_cpu_device_config1_check_py(tmp_path):
     m = json.loads((GOLD / "oracle" / "128x128.json").read_text())
     assert reynolds == pytest.approx(m["reynolds_last_av"], rel=1e-5)
     assert "MLUPS" in out
+
+
+@pytest.mark.parametrize("opt", [["--tolerance"], ["--kernel", "stream"], ["--spl", "4"], ["-n", "4"],
+                                 ["--graph-steps", "8"]])
+def test_cpu_device_refuses_gpu_only_options(tmp_path, opt):
+    """--device cpu has one numerics and one kernel: a '--device cpu --tolerance'
+    run must fail loudly instead of writing bitwise results."""
+    r = subprocess.run([str(EXE), "--device", "cpu", "--params", str(GOLD / "params" / "input_128x128.params"),
+                        "--obstacles", str(GOLD / "params" / "obstacles_128x128.dat"), "--runs", "0",
+                        "--out-dir", str(tmp_path)] + opt, capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert "GPU-only" in r.stderr and opt[0] in r.stderr
+    assert not (tmp_path / "av_vels.dat").exists()

@@ -52,7 +52,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variant", action="append", default=[])
     ap.add_argument("--check", action="store_true", help="also compare each variant's lattice to the first")
+    ap.add_argument("--maps", default="", help="write /proc/self/maps to this file at interpreter exit "
+                    "(maps the PCs of a crash in the C exit handlers, which run after it)")
     a = ap.parse_args()
+    if a.maps:
+        import atexit
+        import shutil
+        atexit.register(shutil.copyfile, "/proc/self/maps", a.maps)
     nx, ny = a.n, a.ny or a.n
     p = lio.Params(nx, ny, a.steps, 10, 0.1, 0.005, 1.85)
     obst = synthetic_obstacles(nx, ny)
