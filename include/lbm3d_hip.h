@@ -42,7 +42,7 @@
  * Placement reuses lbm_config (lbm_hip.h): parts = z slabs, transport LOCAL
  * (all slabs in this process, device copies) or RCCL (one slab per rank);
  * kernel / graph fields are ignored; flags may carry LBM_FLAG_TOLERANCE: the
- * two- and three-step passes then use the reciprocal collision (one v_rcp_f32 + Newton
+ * two- and three-step passes then use the reciprocal collision (one v_rcp_f32 without a Newton
  * step for u, FMA contraction; not bitwise equal to the restatement, within
  * the tolerance tests/test_d3q19.py states), one-step launches stay bitwise.
  */

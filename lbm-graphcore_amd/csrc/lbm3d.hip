@@ -223,7 +223,7 @@ __device__ __forceinline__ float cell3d(const float (&s)[Q3], float (&o)[Q3], bo
 }
 
 // LBM_FLAG_TOLERANCE form of cell3d (the 2-D collide2t's reassociation in
-// 3-D): one reciprocal of rho (v_rcp_f32 + a Newton step) for the velocity,
+// 3-D): one reciprocal of rho (v_rcp_f32, 1 ulp, no Newton step) for the velocity,
 // carried scaled (v = 3u), rho * (omega / 3 | 18 | 36), and per pair of
 // opposite speeds out_k = fma(s_k, 1 - omega, P) +- Q with P = ld (v^2 / 2 +
 // c), c = 1 - |v|^2 / 6, Q = ld v (+ the body-force weight of the pair, which
@@ -255,8 +255,7 @@ __device__ __forceinline__ float cell3dt(const float (&s)[Q3], float (&o)[Q3], b
     const float az = s[9] + s[10] + s[11] + s[12] + s[13], bz = s[14] + s[15] + s[16] + s[17] + s[18];
     // ax + bx holds speeds 1, 2, 5-8, 10, 11, 15, 16; the rest of the 19 here
     const float rho = ((s[0] + (s[3] + s[4])) + (ax + bx)) + ((s[9] + s[12] + s[13]) + (s[14] + s[17] + s[18]));
-    float r = __builtin_amdgcn_rcpf(rho);
-    r = __builtin_fmaf(r, __builtin_fmaf(-rho, r, 1.00f), r);
+    const float r = __builtin_amdgcn_rcpf(rho);
     const float r3 = r * 3.00f;
     const float vx = (ax - bx) * r3, vy = (ay - by) * r3, vz = (az - bz) * r3;  // 3 u
     const float h = __builtin_fmaf(vx, vx, __builtin_fmaf(vy, vy, vz * vz));   // 9 |u|^2

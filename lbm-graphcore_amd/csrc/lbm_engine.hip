@@ -250,7 +250,13 @@ struct lbm_handle {
     int res_per_cu = 1;      // LBM_RES_PER_CU: tiles per CU the choice may plan for (1 or 2)
     int res_early_poll = 0;  // LBM_RES_EARLY: v2 polls the ring after its first work item
     int res_version = 0;     // LBM_RES_V: 1 scalar 64-col tiles, 2 packed 128-col; 0 = by grid
-    bool res_coop = true;    // LBM_RES_COOP: cooperative launch of the resident kernel (else a plain one)
+    // LBM_RES_COOP=1: launch the resident kernel with hipLaunchCooperativeKernel.
+    // Default: a plain launch of the occupancy-sized grid.  A process that had
+    // made a cooperative launch died in exit() under rocprofv3 (SIGSEGV in
+    // libhsa-runtime64 under libamdhip64's exit-time teardown, after the
+    // profiler's finalisation, on a device-mapped page; no frame of this
+    // library): profiles/r05/exitseg/, DESIGN.md section 4.4.
+    bool res_coop = false;
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
     float *res_partials = nullptr;

@@ -174,10 +174,10 @@ __device__ __forceinline__ f2 collide2u(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
 }
 
 // LBM_FLAG_TOLERANCE collision: the same BGK step as collide2u, reassociated
-// for fewer VALU instructions (56 packed + 2 v_rcp_f32 per cell pair against
+// for fewer VALU instructions (54 packed + 2 v_rcp_f32 per cell pair against
 // 95 packed + 63 scalar in the bitwise form).  Not bitwise equal to
 // LastChance.cpp:226-262 -- within the tolerance lbm_hip.h states:
-//   * 1/rho once per cell (v_rcp_f32, 1 ulp, plus one Newton step), shared by
+//   * 1/rho once per cell (v_rcp_f32, 1 ulp; round 5 dropped the Newton step), shared by
 //     u_x and u_y, instead of two correctly rounded divisions; the velocities
 //     are carried scaled, v = 3u = (m / rho) * 3;
 //   * rho/9 * omega and rho/36 * omega as rho * (omega/9), rho * (omega/36);
@@ -201,7 +201,9 @@ __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
     const f2 c = s[2] + s[5] + s[6], d = s[4] + s[7] + s[8];
     const f2 rho = (s[0] + s[2] + s[4]) + (a + b);
     f2 r = f2{__builtin_amdgcn_rcpf(rho.x), __builtin_amdgcn_rcpf(rho.y)};
-    r = fma2(r, fma2(-rho, r, mk2(1.00f)), r);  // one Newton step: ~0.5 ulp
+    // (no Newton step: the hardware reciprocal's 1 ulp is inside the stated
+    // tolerance, and dropping the two packed FMAs per cell pair and level ran
+    // the S = 10 launch 2.6 % faster, profiles/r05/ab/)
     const f2 r3 = r * mk2(3.00f);
     const f2 vx = (a - b) * r3, vy = (c - d) * r3;  // 3 u
     const f2 hx = vx * vx, hy = vy * vy;

@@ -345,7 +345,7 @@ int main(int argc, char *argv[]) {
                       << lbm_steps_per_launch(h) << " steps, " << single_l << " one-step)" << std::endl;
             std::cout << "HBM GB/s per lattice pass: " << std::fixed << std::setprecision(1) << pass_gbs << " = "
                       << std::setprecision(1) << 100.0 * pass_gbs / HBM_PEAK_GBS << " % of the "
-                      << HBM_PEAK_GBS << " GB/s HBM roofline" << std::endl;
+                      << (int)HBM_PEAK_GBS << " GB/s HBM roofline" << std::endl;
         }
     }
     std::vector<lbm_kernel_time> prof;
