@@ -213,29 +213,30 @@ __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
     const f2 omo = mk2(k.omo);
     const f2 half = mk2(0.50f);
     f2 cc[Q];
+    // the four pairs' chains written stage by stage, not pair by pair:
+    // consecutive packed instructions are then independent, where the
+    // pair-by-pair order made the compiler place them back to back and pad
+    // each dependent pair with an s_nop (81 -> 3 in the S = 10 LP loop,
+    // 244 -> 254 VGPRs; S = 10 launch -2 %, S = 8 -10 %, the same lattice bit
+    // for bit: profiles/r05/ab/ab_ilv.log)
+    const f2 ws = vx + vy, wd = vy - vx;
+    const f2 w5 = ws * ws, w6 = wd * wd;
+    const f2 q1 = fma2(hx, half, csq), q2 = fma2(hy, half, csq);
+    const f2 q5 = fma2(w5, half, csq), q6 = fma2(w6, half, csq);
+    const f2 p1 = ld1 * q1, p2 = ld1 * q2, p5 = ld2 * q5, p6 = ld2 * q6;
+    const f2 t1 = fma2(s[1], omo, p1), t2 = fma2(s[2], omo, p2), t5 = fma2(s[5], omo, p5),
+             t6 = fma2(s[6], omo, p6);
+    const f2 t3 = fma2(s[3], omo, p1), t4 = fma2(s[4], omo, p2), t7 = fma2(s[7], omo, p5),
+             t8 = fma2(s[8], omo, p6);
     cc[0] = fma2(s[0], omo, (rho * mk2(k.c0)) * csq);
-    {
-        const f2 p = ld1 * fma2(hx, half, csq);
-        cc[1] = fma2(ld1, vx, fma2(s[1], omo, p));
-        cc[3] = fma2(-ld1, vx, fma2(s[3], omo, p));
-    }
-    {
-        const f2 p = ld1 * fma2(hy, half, csq);
-        cc[2] = fma2(ld1, vy, fma2(s[2], omo, p));
-        cc[4] = fma2(-ld1, vy, fma2(s[4], omo, p));
-    }
-    {
-        const f2 ws = vx + vy;
-        const f2 p = ld2 * fma2(ws * ws, half, csq);
-        cc[5] = fma2(ld2, ws, fma2(s[5], omo, p));
-        cc[7] = fma2(-ld2, ws, fma2(s[7], omo, p));
-    }
-    {
-        const f2 wd = vy - vx;
-        const f2 p = ld2 * fma2(wd * wd, half, csq);
-        cc[6] = fma2(ld2, wd, fma2(s[6], omo, p));
-        cc[8] = fma2(-ld2, wd, fma2(s[8], omo, p));
-    }
+    cc[1] = fma2(ld1, vx, t1);
+    cc[2] = fma2(ld1, vy, t2);
+    cc[5] = fma2(ld2, ws, t5);
+    cc[6] = fma2(ld2, wd, t6);
+    cc[3] = fma2(-ld1, vx, t3);
+    cc[4] = fma2(-ld1, vy, t4);
+    cc[7] = fma2(-ld2, ws, t7);
+    cc[8] = fma2(-ld2, wd, t8);
     if (accrow) {
         // a real (wave-uniform) branch: without this barrier to speculation
         // the compiler if-converts it into 6 adds + 12 selects on EVERY row
