@@ -195,6 +195,12 @@ struct TolK {
     float omo, c0, c1, c2;
 };
 constexpr float TOL_USQ_ROOT = 1.00f / 3.00f;
+// STAGED (the stream kernel): the speed pairs stage by stage (below);
+// false (the resident tiles, 16 waves per CU = 128 VGPRs): pair by pair --
+// the staged order holds more values at once and spilled 7 VGPRs there
+// (1024^2 tolerance 240 vs 262 GLUPS).  The same operations either way: the
+// two orders give the same lattice bit for bit.
+template <bool STAGED = true>
 __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, bool ob, bool any_obst, bool accrow,
                                         const TolK &k, float w1, float w2) {
     const f2 a = s[1] + s[5] + s[8], b = s[3] + s[6] + s[7];
@@ -219,6 +225,31 @@ __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
     // each dependent pair with an s_nop (81 -> 3 in the S = 10 LP loop,
     // 244 -> 254 VGPRs; S = 10 launch -2 %, S = 8 -10 %, the same lattice bit
     // for bit: profiles/r05/ab/ab_ilv.log)
+    if constexpr (!STAGED) {
+        cc[0] = fma2(s[0], omo, (rho * mk2(k.c0)) * csq);
+        {
+            const f2 p = ld1 * fma2(hx, half, csq);
+            cc[1] = fma2(ld1, vx, fma2(s[1], omo, p));
+            cc[3] = fma2(-ld1, vx, fma2(s[3], omo, p));
+        }
+        {
+            const f2 p = ld1 * fma2(hy, half, csq);
+            cc[2] = fma2(ld1, vy, fma2(s[2], omo, p));
+            cc[4] = fma2(-ld1, vy, fma2(s[4], omo, p));
+        }
+        {
+            const f2 ws = vx + vy;
+            const f2 p = ld2 * fma2(ws * ws, half, csq);
+            cc[5] = fma2(ld2, ws, fma2(s[5], omo, p));
+            cc[7] = fma2(-ld2, ws, fma2(s[7], omo, p));
+        }
+        {
+            const f2 wd = vy - vx;
+            const f2 p = ld2 * fma2(wd * wd, half, csq);
+            cc[6] = fma2(ld2, wd, fma2(s[6], omo, p));
+            cc[8] = fma2(-ld2, wd, fma2(s[8], omo, p));
+        }
+    } else {
     const f2 ws = vx + vy, wd = vy - vx;
     const f2 w5 = ws * ws, w6 = wd * wd;
     const f2 q1 = fma2(hx, half, csq), q2 = fma2(hy, half, csq);
@@ -237,6 +268,7 @@ __device__ __forceinline__ f2 collide2t(const f2 (&s)[Q], f2 (&o)[Q], bool oa, b
     cc[4] = fma2(-ld1, vy, t4);
     cc[7] = fma2(-ld2, ws, t7);
     cc[8] = fma2(-ld2, wd, t8);
+    }
     if (accrow) {
         // a real (wave-uniform) branch: without this barrier to speculation
         // the compiler if-converts it into 6 adds + 12 selects on EVERY row

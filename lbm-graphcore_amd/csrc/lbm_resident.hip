@@ -506,7 +506,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
             f2 u;
             if constexpr (TOL) {
                 const bool oab = (oa >> it) & 1u, obb = (ob >> it) & 1u;
-                const f2 usq = collide2t(s[it], o, oab, obb, (anyo >> it) & 1u, accf != 0.00f,
+                const f2 usq = collide2t<false>(s[it], o, oab, obb, (anyo >> it) & 1u, accf != 0.00f,
                                          TolK{a.omo, a.tc0, a.tc1, a.tc2}, a.w1, a.w2);
                 u = f2{oab ? 0.f : sqrt_av(usq.x), obb ? 0.f : sqrt_av(usq.y)};
             } else {
