@@ -133,6 +133,32 @@ def log(msg: str) -> None:
     print(msg, file=sys.stderr, flush=True)
 
 
+def measure_copy_gbs(nbytes: int, local_rank: int, reps: int = 5) -> dict:
+    """Context for the roofline: a device-to-device copy of one
+    lattice's bytes on this GPU, now (torch copy_: read + write = 2 x nbytes
+    per copy), best of `reps` after one warm-up.  Never the peak the fractions
+    use -- that stays the 8 TB/s HBM figure."""
+    import torch
+    dev = torch.device("cuda", local_rank)
+    n = nbytes // 4
+    src = torch.ones(n, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    best = float("inf")
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        dst.copy_(src)
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b) * 1e-3)
+    del src, dst
+    torch.cuda.empty_cache()
+    gbs = 2 * n * 4 / best / 1e9
+    return {"gbs": round(gbs, 1), "bytes": 2 * n * 4, "how": "torch copy_ of one lattice (read + write), best of "
+            f"{reps}, live on this box"}
+
+
 def load_traffic(workload_key: str) -> dict:
     """The committed PMC profile of this workload + kernel (tools/pmc_traffic.py):
     per-launch HBM bytes (gfx950-corrected) and, from the SQ pass, the VALU
@@ -231,7 +257,7 @@ def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
     with native.Engine(p, obst, devices=[0], kernel=kernel, flags=flags, steps_per_launch=spl) as e:
         e.load_cells(lio.init_cells(p))
         e.run()                      # first run: warm-up + results
-        _, av = e.store()
+        e_cells, av = e.store()
         e.run()                      # timed re-run (device events), as LbmRunner's readTimer runs
         secs = e.last_run_seconds()
         used = e.kernel_in_use()
@@ -243,7 +269,41 @@ def aux_1024(kernel: int, flags: int, spl: int = 0) -> dict:
     return {"grid": "1024x1024", "steps": p.max_iters, "kernel": used, "numerics": numerics,
             "mlups": round(cells * p.max_iters / secs / 1e6, 1),
             "ms_per_step": round(secs / p.max_iters * 1e3, 5),
-            "reynolds": lio.reynolds_number(p, float(av[-1])), "note": note}
+            "reynolds": lio.reynolds_number(p, float(av[-1])),
+            "check_gate": check_gate_1024(p, obst, e_cells, av), "note": note}
+
+
+def check_gate_1024(p, obst, cells, av) -> dict:
+    """The reference's two-file gate (check/check.py:62-147, lbm_amd/check.py
+    compare) on the first run's results, in memory: av_vels against the
+    reference's check/1024x1024.av_vels.dat, final-state pressure against the
+    committed full-run fixture (tests/golden/oracle/1024x1024.final_state_
+    pressure.npy.gz, data written by make_golden.py; the reference ships no
+    1024^2 final_state).  Also the largest |pressure| difference, 0 in bitwise
+    mode."""
+    import gzip
+    import io as _io
+    from lbm_amd import check as lcheck
+    gold = ROOT / "tests" / "golden"
+    ref_pr = np.load(_io.BytesIO(gzip.decompress(
+        (gold / "oracle" / "1024x1024.final_state_pressure.npy.gz").read_bytes())))
+    _, _, _, pr = lio.macroscopic(p, obst, cells)
+    ny, nx = pr.shape
+    coords = np.stack([np.tile(np.arange(nx), ny), np.repeat(np.arange(ny), nx)], 1).astype(np.float64)
+    # the written files carry %.12e text: compare the values the text round trip would give
+    sim_fs = np.column_stack([coords, np.asarray(pr, np.float64).ravel()])
+    ref_fs = np.column_stack([coords, np.asarray(ref_pr, np.float64).ravel()])
+    ref_av = lcheck.load_av_vels(gold / "check" / "1024x1024.av_vels.dat.gz")
+    sim_av = np.asarray(av, np.float32).astype(np.float64)
+    res = lcheck.compare(ref_av, ref_fs, sim_av, sim_fs, 1.0)
+    out = {"passed": bool(res["passed"]), "tolerance_pct": 1.0,
+           "pressure_max_abs_diff_vs_oracle": float(np.max(np.abs(pr.astype(np.float64) - ref_pr)))}
+    if "av" in res:
+        out["av_max_diff_pct"] = float(f"{res['av']['max_diff_pcnt']:.3g}")
+        out["final_state_max_diff_pct"] = float(f"{res['fs']['max_diff_pcnt']:.3g}")
+    else:
+        out["reason"] = res["reason"]
+    return out
 
 
 def aux_strong_16384(steps: int, rank: int, world: int, local_rank: int, dist_on: bool, slabs: bool = False,
@@ -894,6 +954,11 @@ def main() -> int:
     fracs = {"hbm": max(frac_pass, frac_counter or 0.0), "valu": frac_valu or 0.0}
     top = max(fracs, key=fracs.get)
     bound = top if fracs[top] >= BOUND_FRAC else "latency"
+    try:
+        copy = measure_copy_gbs(BYTES_PER_UPDATE // 2 * cells_per_gpu, local_rank)
+        copy["pass_vs_copy"] = round(achieved / copy["gbs"], 4)
+    except Exception as exc:  # context only: recorded, never fatal
+        copy = {"error": f"{type(exc).__name__}: {exc}"}
 
     out = {
         "metric": METRIC,
@@ -929,7 +994,9 @@ def main() -> int:
                      "effective_gbs": round(effective, 1),
                      "effective_frac": round(effective / HBM_PEAK_GBS, 4),
                      # VALU instructions per launch and the pipe's busy fraction, same profile
-                     "valu": prof.get("valu") or None, "profile": prof.get("profile")},
+                     "valu": prof.get("valu") or None, "profile": prof.get("profile"),
+                     # what a plain device copy of the same bytes reaches on this box, now
+                     "device_copy": copy},
         "av_vels_finite": m["finite"],
         "numerics": m["numerics"],
         "launches": {"fused": m["launches"][0], "one_step": m["launches"][1],

@@ -44,3 +44,24 @@ def test_pick_spl_follows_a_calibration_table():
     assert bench.pick_spl(18, 0, "tolerance", table=slow10) == 9          # 2 x 9
     json_keys = {"ms": {**{str(S): 1.0 for S in range(2, 6)}, "6": 1.4}, "one_step_ms": 0.8}   # keys after a JSON trip
     assert bench.pick_spl(20, 0, "bitwise", table=json_keys) == 5
+
+
+def test_config2_check_gate_glue(monkeypatch):
+    """bench.check_gate_1024 wiring (CPU): fed the oracle's own full-run
+    pressure and the reference av_vels it passes with zero difference; a
+    perturbed pressure field fails the 1 % gate."""
+    import gzip
+    import io as _io
+    import numpy as np
+    from lbm_amd import check as lcheck
+    gold = ROOT / "tests" / "golden"
+    pr = np.load(_io.BytesIO(gzip.decompress((gold / "oracle" / "1024x1024.final_state_pressure.npy.gz").read_bytes())))
+    av = lcheck.load_av_vels(gold / "check" / "1024x1024.av_vels.dat.gz").astype(np.float32)
+    monkeypatch.setattr(bench.lio, "macroscopic", lambda p, o, c: (None, None, None, pr))
+    g = bench.check_gate_1024(None, None, None, av)
+    assert g["passed"] and g["pressure_max_abs_diff_vs_oracle"] == 0.0, g
+    bad = pr.copy()
+    bad[100, 200] *= 1.05
+    monkeypatch.setattr(bench.lio, "macroscopic", lambda p, o, c: (None, None, None, bad))
+    g = bench.check_gate_1024(None, None, None, av)
+    assert not g["passed"] and abs(g["final_state_max_diff_pct"]) > 1.0, g

@@ -48,6 +48,26 @@ def test_bench_json_contract():
     # value (whole-job MLUPS) and ms_per_step describe the same timed region
     assert d["value"] == pytest.approx(8192 * 8192 / (d["ms_per_step"] * 1e-3) / 1e6, rel=2e-3)
     assert d["av_vels_finite"] is True
+    c = r["device_copy"]   # live context figure: a copy of the same bytes on this box
+    assert 1000 < c["gbs"] < 8000 and c["pass_vs_copy"] == pytest.approx(r["achieved"] / c["gbs"], rel=1e-2)
+
+
+@pytest.mark.parametrize("tolerance", [False, True])
+def test_bench_config2_check_gate(gpu_lib, tolerance):
+    """BASELINE config 2 as the bench reports it (aux config2_1024x1024): all
+    20 000 steps, then the reference's two-file gate in memory -- passes in
+    both numerics, and the final pressure equals the oracle's bit for bit in
+    bitwise mode."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    flags = gpu_lib.FLAG_TOLERANCE if tolerance else 0
+    d = bench.aux_1024(gpu_lib.KERNEL_AUTO, flags)
+    g = d["check_gate"]
+    assert d["steps"] == 20000 and g["passed"], g
+    if tolerance:
+        assert abs(g["final_state_max_diff_pct"]) < 0.1 and abs(g["av_max_diff_pct"]) < 0.1, g
+    else:
+        assert g["pressure_max_abs_diff_vs_oracle"] == 0.0, g
 
 
 def test_bench_bitwise_numerics_line():
