@@ -58,7 +58,9 @@ profile of this workload + kernel exists, else null.  effective_gbs = 72 B x
 cell updates / s (SURVEY 8(d)'s MLUPS x 72 B form), which exceeds the HBM
 peak once temporal blocking pays.  roofline.valu = VALU instructions per
 launch and the VALU pipe's busy fraction from the SQ pass of the same profile
-(tools/pmc_traffic.py --sq).  roofline.bound: "hbm" when frac or
+(tools/pmc_traffic.py --sq).  roofline.device_copy: a device copy of one
+lattice's bytes timed live on this GPU (context; never the
+peak).  roofline.bound: "hbm" when frac or
 frac_counter_bytes (the PMC bytes over the same launch time) reaches 0.75,
 "valu" when frac_valu_issue (VALU busy in quad-cycle units) does -- the larger
 wins -- and "latency" when none does (the launch waits on loads, LDS and
@@ -416,8 +418,9 @@ D3Q19_STEPS = 60
 
 def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_on: bool, flags: int = 0) -> dict:
     """BASELINE config 5: D3Q19 n^3 channel (body force between wall planes y = 0 and
-    y = n-1), z slabs over all ranks (RCCL: two ghost planes each way per
-    two-step pass, overlapped with the slab interior), whole-job MLUPS (strong
+    y = n-1), z slabs over all ranks (the engine's default three-step passes:
+    RCCL sends three ghost planes each way per pass, overlapped with the slab
+    interior), whole-job MLUPS (strong
     scaling: the global grid is fixed).  Untimed settle steps (>= 0.2 s of
     device time) precede the timed steps.  No reference counterpart: parity
     pinned only by the CPU restatement (tests/test_d3q19.py)."""
