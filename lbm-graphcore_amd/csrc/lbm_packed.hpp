@@ -42,6 +42,22 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane + 1
 __device__ __forceinline__ f2 left2(f2 v) { return f2{dpp_from_left(v.y), v.x}; }
 __device__ __forceinline__ f2 right2(f2 v) { return f2{v.y, dpp_from_right(v.x)}; }
 
+// The same shifts in place: the shifted pair is kept SWAPPED in its registers
+// ({B', A'} for the in-order {A', B'} above), so the half that stays is
+// already where it belongs and the shift is one DPP move over the other half
+// (the in-order forms cost a DPP move plus a copy of the staying half).
+// Readers take it through unswap(), which the packed instructions absorb as
+// op_sel (free); the empty asm keeps the swapped pair in one register pair
+// (without it the element picks cancel before register allocation and the
+// copy comes back).
+__device__ __forceinline__ f2 pin2(f2 v) {
+    asm("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ f2 left2x(f2 v) { return pin2(f2{v.x, dpp_from_left(v.y)}); }
+__device__ __forceinline__ f2 right2x(f2 v) { return pin2(f2{dpp_from_right(v.x), v.y}); }
+__device__ __forceinline__ f2 unswap(f2 u) { return __builtin_shufflevector(u, u, 1, 0); }
+
 // RN(x / d) for d = 9 or 36 (see header)
 template <int D>
 __device__ __forceinline__ f2 div_const(f2 x) {

@@ -22,6 +22,18 @@
 
 #include "lbm_packed.hpp"
 
+// The x-shifted planes the levels keep (rows of planes 1, 3, 5, 6, 7, 8) are
+// held swapped, shifted in place (lbm_packed.hpp left2x); 0 builds the
+// in-order form (tools/build_variant.sh, A/B only).
+#ifndef LBM_SWAP_SHIFT
+#define LBM_SWAP_SHIFT 1
+#endif
+namespace lbm {
+__device__ __forceinline__ f2 shl_kept(f2 v) { return LBM_SWAP_SHIFT ? left2x(v) : left2(v); }
+__device__ __forceinline__ f2 shr_kept(f2 v) { return LBM_SWAP_SHIFT ? right2x(v) : right2(v); }
+__device__ __forceinline__ f2 kept(f2 u) { return LBM_SWAP_SHIFT ? unswap(u) : u; }
+}  // namespace lbm
+
 namespace lbm {
 
 // halo_out with the destinations read from device memory inside the (rare)
@@ -188,26 +200,26 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
             // LP: the registers hold row y-1 of planes 2, 5, 6 (the older row),
             // the LDS slot row y; both move on after the collision (below)
             s[2] = st.p2[0][b];
-            s[5] = st.p5[0][b];
-            s[6] = st.p6[0][b];
+            s[5] = kept(st.p5[0][b]);
+            s[6] = kept(st.p6[0][b]);
         } else {
             s[2] = st.p2[PAR][b];
-            s[5] = st.p5[PAR][b];
-            s[6] = st.p6[PAR][b];
+            s[5] = kept(st.p5[PAR][b]);
+            s[6] = kept(st.p6[PAR][b]);
             st.p2[PAR][b] = cur[2];
-            st.p5[PAR][b] = left2(cur[5]);
-            st.p6[PAR][b] = right2(cur[6]);
+            st.p5[PAR][b] = shl_kept(cur[5]);
+            st.p6[PAR][b] = shr_kept(cur[6]);
         }
         s[0] = st.c0[b];
-        s[1] = st.c1[b];
-        s[3] = st.c3[b];
+        s[1] = kept(st.c1[b]);
+        s[3] = kept(st.c3[b]);
         s[4] = cur[4];
-        s[7] = right2(cur[7]);
-        s[8] = left2(cur[8]);
+        s[7] = kept(shr_kept(cur[7]));
+        s[8] = kept(shl_kept(cur[8]));
         if constexpr (!LP) {
             st.c0[b] = cur[0];
-            st.c1[b] = left2(cur[1]);
-            st.c3[b] = right2(cur[3]);
+            st.c1[b] = shl_kept(cur[1]);
+            st.c3[b] = shr_kept(cur[3]);
         }
         // inputs of this row were never loaded: the result is unused.  The LP
         // forms skip only the collision (the level's inputs still pass
@@ -252,11 +264,11 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
             st.p5[0][b] = slot[64];
             st.p6[0][b] = slot[128];
             slot[0] = cur[2];
-            slot[64] = left2(cur[5]);
-            slot[128] = right2(cur[6]);
+            slot[64] = shl_kept(cur[5]);
+            slot[128] = shr_kept(cur[6]);
             st.c0[b] = cur[0];
-            st.c1[b] = left2(cur[1]);
-            st.c3[b] = right2(cur[3]);
+            st.c1[b] = shl_kept(cur[1]);
+            st.c3[b] = shr_kept(cur[3]);
         }
         const bool rowlive = (!GUARD || y >= g.yo0) && (L == S || y < g.yo1);
         if (rowlive) {
