@@ -157,12 +157,12 @@ __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2
 // instead of registers -- lpl points at this lane's slot of a per-wave
 // [S][3][64] f2 array; each level reads row y-1 from it and writes row y
 // back (the same lane, the same address: no barrier, LDS keeps a wave's
-// order) -- 6 VGPRs fewer per level -- and the per-level |u| sums follow it
-// ([S][64], .x): S VGPRs fewer.  Tolerance forms fit S = 8 at two waves per
-// SIMD, the bitwise form S = 6.
+// order) -- 6 VGPRs fewer per level.  (Rounds 3-4 kept the per-level |u|
+// sums there too, S VGPRs fewer; once the in-place shifts freed 32 VGPRs,
+// registers ran the S = 10 launch 2.5 % faster, profiles/r05/swap/us2_*.)
 template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL, bool LP>
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j,
-                                             const TolK &tk, f2 *lpl, float *lps) {
+                                             const TolK &tk, f2 *lpl) {
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
     // (LP forms issue row j+1's loads later, at level 2: see below)
     if (PD == 1 && !LP) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
@@ -229,12 +229,6 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         // vs 254)
         const bool cold = GUARD && j < g.j0 + 2 * L;
         if (!LP && cold) continue;
-        // LP: this level's running |u| sum is read from LDS here, before the
-        // collision, and added to after it: read right before its use (as the
-        // plain `lps[] +=` compiles), its lgkmcnt(0) wait stalled the wave
-        // once per level for a full LDS round trip
-        float usum = 0.f;
-        if constexpr (LP) usum = lps[b * 64];
 
         f2 o[Q];
         const bool oa = OBST && ((st.oba >> L) & 1u), ob = OBST && ((st.obb >> L) & 1u);
@@ -274,12 +268,7 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         if (rowlive) {
             const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
             const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
-            if constexpr (LP)
-                lps[b * 64] = usum + (ua + ub);  // LP: the per-level |u| sums in LDS, not VGPRs (as an LDS
-                                                 // float atomic add with no return: 1.6x slower,
-                                                 // profiles/r04/ab_libs.log)
-            else
-                st.tot[b] += ua + ub;
+            st.tot[b] += ua + ub;
         }
         if (L == S) {
             if (rowlive && (g.owna || g.ownb)) {
@@ -356,8 +345,8 @@ __device__ __forceinline__ Stream2Geo stream2d_geo(const StreamArgs &a, int t, i
 // (S = 10: 253 VGPRs without spills one row per iteration; 256 + 221 spilled
 // two rows per iteration).
 template <int S, int PD, bool NT, bool OBST, bool TOL, bool LP>
-__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st, f2 *lpl,
-                                              float *lps) {
+__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st,
+                                              f2 *lpl) {
     const Stream2Geo g = stream2d_geo<S>(a, t, lane);
     const TolK tk{a.omo, a.tc0, a.tc1, a.tc2};
     if constexpr (LP) {
@@ -378,21 +367,21 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     int j = g.j0;
     if constexpr (LP) {
 #pragma unroll 1
-        for (int i = 0; i < 2 * S; ++i, ++j) stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
+        for (int i = 0; i < 2 * S; ++i, ++j) stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
 #pragma unroll 1
-        for (; j <= g.jlast; ++j) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
+        for (; j <= g.jlast; ++j) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
     } else {
 #pragma unroll 1
         for (int i = 0; i < S; ++i, j += 2) {
-            stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
-            stream2d_row<S, 1, true, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl, lps);
+            stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
+            stream2d_row<S, 1, true, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl);
         }
 #pragma unroll 1
         for (; j + 1 <= g.jlast; j += 2) {
-            stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
-            stream2d_row<S, 1, false, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl, lps);
+            stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
+            stream2d_row<S, 1, false, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl);
         }
-        if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl, lps);
+        if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
     }
 }
 
@@ -431,8 +420,7 @@ template <int S, bool kReduce, int W, bool NT, bool TOL = false, bool LP = false
 __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     __shared__ float lds[W];
     __shared__ f2 lds_p[LP ? W * 3 * S * 64 : 1];   // LP: [wave][S][3][64] older rows of planes 2, 5, 6
-    __shared__ float lds_u[LP ? W * S * 64 : 1];    // LP: [wave][S][64] |u| sums
-    // (S = 10: 17.5 KB per one-wave workgroup, so eight fit a CU's 160 KB)
+    // (S = 10: 15 KB per one-wave workgroup, so eight fit a CU's 160 KB)
     if (kReduce && blockIdx.x == 0) reduce_pending_n<64 * W>(a.ctl, a.partials_prev, a.av_local, lds);
 
     const int lane = threadIdx.x & 63;
@@ -440,11 +428,6 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
 #pragma unroll
     for (int l = 0; l < S; ++l) st.tot[l] = 0.f;
     f2 *const lpl = lds_p + (LP ? (threadIdx.x >> 6) * 3 * S * 64 : 0) + lane;
-    float *const lps = lds_u + (LP ? (threadIdx.x >> 6) * S * 64 : 0) + lane;
-    if constexpr (LP) {
-#pragma unroll
-        for (int l = 0; l < S; ++l) lps[l * 64] = 0.f;
-    }
     // wave-uniform: keeps the unit geometry and the row loop in scalar registers
     const int slot = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * W + (int)(threadIdx.x >> 6));
     // dispatch order -> work unit (a.uperm: per XCD range, obstacle-bearing
@@ -458,13 +441,9 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
         // read no obstacle cell run the select-free copy of the unit loop
         typedef const __attribute__((address_space(4))) uint8_t CU8;
         if (a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0)
-            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lpl, lps);
+            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lpl);
         else
-            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lpl, lps);
-    }
-    if constexpr (LP) {
-#pragma unroll
-        for (int l = 0; l < S; ++l) st.tot[l] = lps[l * 64];
+            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lpl);
     }
     if (t < max(a.total, 1)) stream2d_partials<S, TOL>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
