@@ -117,6 +117,7 @@ struct Stream2State {
     f2 c0[S], c1[S], c3[S];          // planes 0, 1, 3 of row y (level L input)
     f2 p2[2][S], p5[2][S], p6[2][S]; // [parity]: planes 2, 5(left2), 6(right2) of rows y-1 / y
     float tot[S];                    // per level: running sum of |u| over the wave's owned cells
+    f2 tot2[S];                      // OBST = false units: the same per column, all lanes (masked at the end)
     f2 v[2][Q];                      // [parity]: input row j (parity of j) / prefetched row j+1
     unsigned ob[2][2];               // [parity][A/B]: obstacle bytes of those rows
     unsigned oba, obb;               // per-lane obstacle bits of the last rows (bit L = row j-L)
@@ -266,9 +267,19 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         }
         const bool rowlive = (!GUARD || y >= g.yo0) && (L == S || y < g.yo1);
         if (rowlive) {
-            const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
-            const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
-            st.tot[b] += ua + ub;
+            if constexpr (OBST) {
+                const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
+                const float ub = (ob || !g.ownb) ? 0.f : sqrt_av(usq.y);
+                st.tot[b] += ua + ub;
+            } else {
+                // no obstacle cell in the unit: the lane's column ownership is
+                // the unit's, applied once at its end (stream2d_unit) -- one
+                // packed add per level instead of two selects and two adds
+                // (the empty asm keeps `rowlive` a branch: if-converted, the
+                // sums would cost two selects per level again)
+                asm volatile("");
+                st.tot2[b] += f2{sqrt_av(usq.x), sqrt_av(usq.y)};
+            }
         }
         if (L == S) {
             if (rowlive && (g.owna || g.ownb)) {
@@ -361,6 +372,10 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
     }
     st.oba = st.obb = 0;
     st.rob = 0;
+    if constexpr (!OBST) {
+#pragma unroll
+        for (int b = 0; b < S; ++b) st.tot2[b] = mk2(0.f);
+    }
     stream2d_load<PD, OBST>(a, g, g.j0, st.v[0], st.ob[0]);
     if (PD == 2) stream2d_load<PD, OBST>(a, g, g.j0 + 1, st.v[1], st.ob[1]);
     // warm-up: rows j0 .. j0+2S-1 (level L valid from j0+2L); jlast >= j0+2S
@@ -382,6 +397,10 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int la
             stream2d_row<S, 1, false, PD, NT, OBST, TOL, LP>(a, g, st, j + 1, tk, lpl);
         }
         if (j <= g.jlast) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP>(a, g, st, j, tk, lpl);
+    }
+    if constexpr (!OBST) {
+#pragma unroll
+        for (int b = 0; b < S; ++b) st.tot[b] += (g.owna ? st.tot2[b].x : 0.f) + (g.ownb ? st.tot2[b].y : 0.f);
     }
 }
 
