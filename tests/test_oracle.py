@@ -229,3 +229,29 @@ def test_oracle_mt_bitwise():
     b, av_b = oracle.run_mt(p, obst, 40, 4)
     assert np.array_equal(a, b)
     np.testing.assert_allclose(av_b, av_a, rtol=1e-4)  # row-wise partial sums
+
+
+def test_reference_binary_all_obstacles_and_single_column(tmp_path):
+    """The degenerate inputs tests/test_gpu_edge.py runs on the GPU, through
+    the reference's own LastChance: every cell an obstacle gives av_vels of
+    0 / 0 free cells -- NaN -- as the oracle does; a single-column channel
+    (nx = 1, periodic onto itself) matches the oracle's av_vels text exactly."""
+    if not oracle.REF_LASTCHANCE.exists():
+        pytest.skip("oracle/_ref/lastchance not built (reference sources absent)")
+    pf, of = tmp_path / "a.params", tmp_path / "a.dat"
+    pf.write_text("16\n8\n10\n10\n0.1\n0.005\n1.85\n")
+    of.write_text("".join(f"{x} {y} 1\n" for y in range(8) for x in range(16)))
+    (tmp_path / "a").mkdir()
+    ref = oracle.run_reference(str(pf), str(of), str(tmp_path / "a"))
+    ref_av = lcheck.load_av_vels(ref["av_vels"])
+    p = lio.Params.from_file(str(pf))
+    _, av = oracle.run(p, lio.read_obstacles(p.nx, p.ny, str(of)))
+    assert ref_av.size == 10 and np.isnan(ref_av).all() and np.isnan(av).all()
+    pf2, of2 = tmp_path / "c.params", tmp_path / "c.dat"
+    pf2.write_text("1\n12\n40\n10\n0.1\n0.005\n1.85\n")
+    of2.write_text("0 0 1\n0 11 1\n")
+    (tmp_path / "c").mkdir()
+    ref = oracle.run_reference(str(pf2), str(of2), str(tmp_path / "c"))
+    p2 = lio.Params.from_file(str(pf2))
+    _, av2 = oracle.run(p2, lio.read_obstacles(p2.nx, p2.ny, str(of2)))
+    assert open(ref["av_vels"]).read() == "".join(f"{i}:\t{float(v):.12E}\n" for i, v in enumerate(av2))
