@@ -233,6 +233,7 @@ struct lbm_handle {
     int og = 4;              // ghost width of the obstacle map
     std::vector<std::pair<int, float>> guide;  // LBM_STREAM_GUIDE tiers (height, fraction of a band's rows)
     bool guide_set = false;                    // guide given by LBM_STREAM_GUIDE (else by S at create)
+    bool guide_auto = false;                   // the default tiers: only where they fit the rect (tiers_fit)
     int stream_cfg = 4;      // LBM_STREAM_CFG (launch form, one wave per workgroup): 0 plain stores;
                              // 3 non-temporal lattice stores; 4 LP (older rows of planes 2,5,6 in LDS, S <= 10)
     // LBM_TOL_S / LBM_TOL_CFG: steps per launch and form with LBM_FLAG_TOLERANCE
@@ -844,6 +845,8 @@ struct lbm_handle {
         const int y0 = ydec ? b : 0, y1 = ydec ? s.h - b : s.h;
         const int x0 = xdec ? xb : 0, x1 = xdec ? s.w - xb : s.w;
         int hs = stream_hs;
+        long long cap = 0;  // the device's concurrently resident waves of this launch form
+        const long long strips_in = (std::max(x1 - x0, 1) + ow_of(x0) - 1) / ow_of(x0);
         if (hs <= 0) {
             const long long strips = (std::max(x1 - x0, 1) + ow_of(x0) - 1) / ow_of(x0);
             const long long rows = std::max(y1 - y0, 1);
@@ -859,7 +862,7 @@ struct lbm_handle {
             if (occ == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev) == hipSuccess &&
                 per_cu > 0 && cus > 0) {
-                const long long cap = (long long)per_cu * cus;
+                cap = (long long)per_cu * cus;
                 const long long nseg_max = std::max<long long>(1, rows / (4LL * S));
                 const long long k_max = std::max<long long>(1, nseg_max * strips / cap);
                 const long long k = std::min<long long>(8, k_max);
@@ -885,7 +888,8 @@ struct lbm_handle {
             bnd.push_back(mk(s.w - xb, y0, xb, y1 - y0, hs));
         }
         if (x1 > x0 && y1 > y0) {
-            if (!guided_rects(x0, y0, x1 - x0, y1 - y0, mk, inr)) inr.push_back(mk(x0, y0, x1 - x0, y1 - y0, hs));
+            if (!guided_rects(x0, y0, x1 - x0, y1 - y0, mk, inr, strips_in, cap))
+                inr.push_back(mk(x0, y0, x1 - x0, y1 - y0, hs));
         }
     }
 
@@ -899,9 +903,40 @@ struct lbm_handle {
     // (little re-streamed overlap) first, short ones last to fill the tail.
     // LBM_STREAM_GUIDE = "h1:f1,h2:f2,...,hK" (tier heights, fractions of a
     // band's rows; the last tier takes the rest), "0" = uniform heights.
+    // Whether the default tiers suit an h-row rect of `strips` strips: they
+    // were tuned at 8192^2 (3.6 rounds of the device's wave slots at S = 10,
+    // 5.3 at S = 6, the shortest tier taking 6 % of each band); on smaller
+    // rects they cut too few work units to fill the device, or leave a large
+    // share of each band to the shortest tier (4096^2: 34 % in 16-row
+    // segments, each re-streaming 2S = 20 rows).  There the uniform heights
+    // of stream_split's rounds rule serve better (profiles/r05/mid/: 4096^2
+    // tolerance 0.065 -> 0.046 ms per step, 3072^2 0.061 -> 0.028, bitwise
+    // 3072^2 0.081 -> 0.046; 4096 x 8192 and 6144^2 keep the tiers).  Fit:
+    // at least 1.5 rounds (2.5 for the S <= 6 tiers) and at most a quarter of
+    // the rows in the shortest tier.
+    bool tiers_fit(long long strips, int h, long long cap) const {
+        if (!guide_auto || cap <= 0 || guide.empty()) return true;
+        long long segs = 0, last_rows = 0;
+        for (const int rb : round_robin(h, 8)) {
+            int rest = rb;
+            for (size_t k = 0; k < guide.size() && rest > 0; ++k) {
+                const int ht = std::max(1, guide[k].first);
+                int r = rest;
+                if (k + 1 < guide.size()) r = std::min(rest, std::max(ht, (int)(rb * guide[k].second) / ht * ht));
+                segs += (r + ht - 1) / ht;
+                if (k + 1 == guide.size()) last_rows += r;
+                rest -= r;
+            }
+        }
+        const double rounds_min = guide[0].first >= 144 ? 1.5 : 2.5;
+        return (double)(segs * strips) >= rounds_min * (double)cap && 4 * last_rows <= h;
+    }
+
     template <class MK>
-    bool guided_rects(int x0, int y0, int w, int h, MK &&mk, std::vector<SRect> &out) const {
+    bool guided_rects(int x0, int y0, int w, int h, MK &&mk, std::vector<SRect> &out, long long strips,
+                      long long cap) const {
         if (stream_hs > 0 || guide.empty()) return false;
+        if (!tiers_fit(strips, h, cap)) return false;
         constexpr int NB = 8;
         const int hb = h / NB;
         if (hb < 2 * guide[0].first) return false;
@@ -1045,7 +1080,10 @@ struct lbm_handle {
         // default segment tiers by S (2S rows re-streamed per segment): S <= 6
         // 96/32/10 (profiles/r02/ab_guide_tiers.log), S >= 7 144/48/16
         // (profiles/r03/guide7/: 400 vs 390 GLUPS at 98 steps, 385 vs 377 at 20)
-        if (!guide_set) set_guide(spl >= 7 ? "144:0.85,48:0.1,16" : "96:0.85,32:0.1,10");
+        if (!guide_set) {
+            set_guide(spl >= 7 ? "144:0.85,48:0.1,16" : "96:0.85,32:0.1,10");
+            guide_auto = true;
+        }
         gr = std::max(2, hw);
         og = gr + 2;  // the two-column stream kernel's strips start up to S+1 columns left of their first cell
 
