@@ -33,6 +33,10 @@
 #include "lbm3d_hip.h"
 #include "lbm_packed.hpp"
 
+#ifndef LBM3D_XCD_REMAP
+#define LBM3D_XCD_REMAP 1  // 0: the hardware's block order (A/B builds only)
+#endif
+
 namespace lbm {
 
 constexpr int Q3 = 19;
@@ -431,6 +435,25 @@ struct T3 {
     static constexpr int OY = TH - 4;                     // owned rows
 };
 
+// XCD-aware block order for the multi-step passes (as the 2-D stream
+// kernel's xcd_remap, lbm_device.hpp): the hardware deals workgroups to the
+// eight XCDs round robin, so consecutive blocks -- x neighbours, whose
+// windows overlap by six columns, and y neighbours, overlapping by six rows
+// -- landed on different XCDs and read their shared cells from HBM twice.
+// Here each XCD takes one contiguous range of (x fastest, then y, then z)
+// blocks, so neighbours run side by side on one XCD and the overlap comes
+// from its L2.  Blocks keep their logical index for the |u| partials.
+struct Blk3 {
+    int x, y, z;
+};
+__device__ __forceinline__ Blk3 blk3_remap() {
+    const int nb = gridDim.x * gridDim.y * gridDim.z;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int l = LBM3D_XCD_REMAP ? xcd_remap(lin, nb) : lin;
+    const int yz = l / gridDim.x;
+    return Blk3{l - yz * (int)gridDim.x, yz % (int)gridDim.y, yz / (int)gridDim.y};
+}
+
 struct Two3Args {
     const float *fin;   // origin of the lattice read (ghost planes -2, -1, nz, nz + 1 filled)
     float *fout;
@@ -518,13 +541,14 @@ __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
     __shared__ float lds1[T3<TH>::LDS], lds2[T3<TH>::LDS];
     __shared__ float red[2][TH];
     const int lane = threadIdx.x, wy = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    const int ox = blockIdx.x * T3OX, oy = blockIdx.y * T3<TH>::OY;
+    const Blk3 B = blk3_remap();
+    const int ox = B.x * T3OX, oy = B.y * T3<TH>::OY;
     const bool live1 = !SKIP || (wy >= 1 && wy < TH - 1), live2 = !SKIP || (wy >= 2 && wy < TH - 2);
     const int x = (((ox - 2 + lane) % a.nx) + a.nx) % a.nx;
     const int y = (((oy - 2 + wy) % a.ny) + a.ny) % a.ny;
     const bool own = lane >= 2 && lane < T3W - 2 && wy >= 2 && wy < TH - 2 && ox + lane - 2 < a.nx &&
                      oy + wy - 2 < a.ny;
-    const int zs = a.z0 + blockIdx.z * a.seg, ze = min(zs + a.seg, a.zn);
+    const int zs = a.z0 + B.z * a.seg, ze = min(zs + a.seg, a.zn);
     const long long row = (long long)y * a.px + x;
     float r0a[3] = {0.f, 0.f, 0.f}, r9aa[3] = {0.f, 0.f, 0.f}, r9ba[3] = {0.f, 0.f, 0.f};
     float r0b[3] = {0.f, 0.f, 0.f}, r9ab[3] = {0.f, 0.f, 0.f}, r9bb[3] = {0.f, 0.f, 0.f};
@@ -599,7 +623,7 @@ __global__ __launch_bounds__(T3W * TH) void step3d_two(Two3Args a) {
             b1 += red[0][i];
             b2 += red[1][i];
         }
-        const int blk = a.blk0 + (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const int blk = a.blk0 + (B.z * gridDim.y + B.y) * gridDim.x + B.x;
         a.partials[blk] = b1;
         a.partials[a.nblocks + blk] = b2;
     }
@@ -629,12 +653,13 @@ __global__ __launch_bounds__(T3W *T3TH3) void step3d_three(Two3Args a) {
     __shared__ float lds1[T3<T3TH3>::LDS], lds2[T3<T3TH3>::LDS], lds3[T3<T3TH3>::LDS];
     __shared__ float red[3][T3TH3];
     const int lane = threadIdx.x, wy = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    const int ox = blockIdx.x * T3OX3, oy = blockIdx.y * T3OY3;
+    const Blk3 B = blk3_remap();
+    const int ox = B.x * T3OX3, oy = B.y * T3OY3;
     const int x = (((ox - 3 + lane) % a.nx) + a.nx) % a.nx;
     const int y = (((oy - 3 + wy) % a.ny) + a.ny) % a.ny;
     const bool own = lane >= 3 && lane < T3W - 3 && wy >= 3 && wy < T3TH3 - 3 && ox + lane - 3 < a.nx &&
                      oy + wy - 3 < a.ny;
-    const int zs = a.z0 + blockIdx.z * a.seg, ze = min(zs + a.seg, a.zn);
+    const int zs = a.z0 + B.z * a.seg, ze = min(zs + a.seg, a.zn);
     const long long row = (long long)y * a.px + x;
     float r0a[3] = {0.f, 0.f, 0.f}, r9aa[3] = {0.f, 0.f, 0.f}, r9ba[3] = {0.f, 0.f, 0.f};
     float r0b[3] = {0.f, 0.f, 0.f}, r9ab[3] = {0.f, 0.f, 0.f}, r9bb[3] = {0.f, 0.f, 0.f};
@@ -699,7 +724,7 @@ __global__ __launch_bounds__(T3W *T3TH3) void step3d_three(Two3Args a) {
             b2 += red[1][i];
             b3 += red[2][i];
         }
-        const int blk = a.blk0 + (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const int blk = a.blk0 + (B.z * gridDim.y + B.y) * gridDim.x + B.x;
         a.partials[blk] = b1;
         a.partials[a.nblocks + blk] = b2;
         a.partials[2 * a.nblocks + blk] = b3;
