@@ -797,3 +797,30 @@ def test_placement_probe_same_lattice(gpu_lib, transport, monkeypatch):
     assert np.array_equal(out[0][0], out[1][0])
     assert np.array_equal(out[0][1], out[1][1])
     assert np.isfinite(out[1][1]).all()
+
+
+@pytest.mark.parametrize("nx,ny", [(3072, 3072), (4096, 2048), (2048, 4096)])
+def test_mid_size_stream_split(gpu_lib, nx, ny):
+    """Grids where the stream split cuts uniform segment heights instead of
+    the 8192^2 tiers (lbm_engine.hip tiers_fit, round 5): 13 steps = two fused
+    6-step launches + one one-step launch, bitwise vs the oracle; and the
+    tolerance collision (S = 10: one 10-step launch + a fused 3-step
+    remainder) within the 2e-5 bound of tests/test_gpu_tolerance.py."""
+    from test_gpu_tolerance import TOL_POP, _rel
+    p = lio.Params(nx, ny, 13, 10, 0.1, 0.005, 1.85)
+    obst = bench_obstacles(nx) if nx == ny else np.pad(np.zeros((ny - 2, nx - 2), np.uint8), 1, constant_values=1)
+    ref, ref_av = oracle.run_mt(p, obst, 13, 16, lio.init_cells(p))
+    with gpu_lib.Engine(p, obst) as e:
+        assert e.kernel_in_use() == "stream" and e.steps_per_launch() == 6
+        e.init_equilibrium()
+        e.run_steps(13, accelerate_first=True)
+        assert e.run_stats() == (2, 1)
+        cells, av = e.store(n_av=13)
+    assert np.array_equal(cells, ref)
+    np.testing.assert_allclose(av, ref_av, rtol=2e-3)
+    with gpu_lib.Engine(p, obst, flags=gpu_lib.FLAG_TOLERANCE) as e:
+        assert e.kernel_in_use() == "stream" and e.steps_per_launch() == 10
+        e.init_equilibrium()
+        e.run_steps(13, accelerate_first=True)
+        cells, _ = e.store(n_av=13)
+    assert _rel(cells, ref) < TOL_POP
