@@ -29,12 +29,10 @@
 #define LBM_SWAP_SHIFT 1
 #endif
 namespace lbm {
+
 __device__ __forceinline__ f2 shl_kept(f2 v) { return LBM_SWAP_SHIFT ? left2x(v) : left2(v); }
 __device__ __forceinline__ f2 shr_kept(f2 v) { return LBM_SWAP_SHIFT ? right2x(v) : right2(v); }
 __device__ __forceinline__ f2 kept(f2 u) { return LBM_SWAP_SHIFT ? unswap(u) : u; }
-}  // namespace lbm
-
-namespace lbm {
 
 // halo_out with the destinations read from device memory inside the (rare)
 // branch that stores them, so they hold no scalar registers across the loop
@@ -114,8 +112,8 @@ __device__ __forceinline__ void halo_out_g(const StreamArgs &a, int S, int x, in
 //     cell is in it.
 template <int S>
 struct Stream2State {
-    f2 c0[S], c1[S], c3[S];          // planes 0, 1, 3 of row y (level L input)
-    f2 p2[2][S], p5[2][S], p6[2][S]; // [parity]: planes 2, 5(left2), 6(right2) of rows y-1 / y
+    f2 c0[S], c1[S], c3[S];          // planes 0, 1, 3 of row y (level L input; 1, 3 shifted, held swapped)
+    f2 p2[2][S], p5[2][S], p6[2][S]; // [parity]: planes 2, 5, 6 of rows y-1 / y (5, 6 shifted, held swapped)
     float tot[S];                    // per level: running sum of |u| over the wave's owned cells
     f2 tot2[S];                      // OBST = false units: the same per column, all lanes (masked at the end)
     f2 v[2][Q];                      // [parity]: input row j (parity of j) / prefetched row j+1
