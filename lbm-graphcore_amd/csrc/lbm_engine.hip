@@ -70,6 +70,7 @@ hipError_t launch_pipe_av(const float *partials, int n, float *av_local, int t, 
 hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, bool coop, hipStream_t s);
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s);
 hipError_t launch_debug_spin(int microseconds, hipStream_t s);
+hipError_t launch_debug_lds_hog(int milliseconds, int workgroups, float *sink, hipStream_t s);
 }  // namespace lbm
 
 using namespace lbm;
@@ -251,13 +252,22 @@ struct lbm_handle {
     int res_per_cu = 1;      // LBM_RES_PER_CU: tiles per CU the choice may plan for (1 or 2)
     int res_early_poll = 0;  // LBM_RES_EARLY: v2 polls the ring after its first work item
     int res_version = 0;     // LBM_RES_V: 1 scalar 64-col tiles, 2 packed 128-col; 0 = by grid
-    // LBM_RES_COOP=1: launch the resident kernel with hipLaunchCooperativeKernel.
-    // Default: a plain launch of the occupancy-sized grid.  A process that had
-    // made a cooperative launch died in exit() under rocprofv3 (SIGSEGV in
-    // libhsa-runtime64 under libamdhip64's exit-time teardown, after the
-    // profiler's finalisation, on a device-mapped page; no frame of this
-    // library): profiles/r05/exitseg/, DESIGN.md section 4.4.
-    bool res_coop = false;
+    // The resident kernel is launched with hipLaunchCooperativeKernel (the
+    // runtime's admission check of the whole grid).  LBM_RES_COOP=0 (debug
+    // knob) launches it plainly: a process that had made a cooperative launch
+    // died in exit() under rocprofv3 (SIGSEGV in libhsa-runtime64 under
+    // libamdhip64's exit-time teardown, after the profiler's finalisation; no
+    // frame of this library: profiles/r05/exitseg/),
+    // so the profiling scripts set it.  Either way a grid that does not
+    // become co-resident is caught by the poll deadline and the run is
+    // repeated on STEP2 (run_steps, res_failed).
+    bool res_coop = true;
+    bool res_failed = false;        // a resident run timed out: this handle runs STEP2 from then on
+    int res_stall_tile = -1, res_stall_step = 1;  // LBM_DEBUG_RES_STALL_TILE / _STEP
+    int res_timeout_ms = 2000;      // LBM_DEBUG_RES_TIMEOUT_MS: poll deadline
+    int res_hog_ms = 0, res_hog_wgs = 0;  // LBM_DEBUG_RES_HOG_MS / _WGS: LDS hog beside the launch
+    hipStream_t res_hog_stream = nullptr;
+    float *res_hog_sink = nullptr;
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
     float *res_partials = nullptr;
@@ -320,11 +330,19 @@ struct lbm_handle {
             f();
             return;
         }
-        ProfRec r{prof_class(cls), s.dev, prof_event(s.dev), prof_event(s.dev)};
+        // the record is listed before anything can throw, so a failed launch
+        // returns its two events to the pool (prof_drop at the next run)
+        ProfRec r{prof_class(cls), s.dev, prof_event(s.dev), nullptr};
+        try {
+            r.b = prof_event(s.dev);
+        } catch (...) {
+            prof_pool.push_back({s.dev, r.a});
+            throw;
+        }
+        prof_open.push_back(r);
         HIP_CHECK(hipEventRecord(r.a, st));
         f();
         HIP_CHECK(hipEventRecord(r.b, st));
-        prof_open.push_back(r);
     }
     // after a run's streams are synchronised: fold this run's records
     void prof_collect() {
@@ -457,12 +475,22 @@ struct lbm_handle {
         res_th_env = std::max(0, knob("LBM_RES_TH", 0));
         res_version = knob("LBM_RES_V", 0);
         res_coop = knob("LBM_RES_COOP", res_coop ? 1 : 0) != 0;
+        res_stall_tile = knob("LBM_DEBUG_RES_STALL_TILE", -1);
+        res_stall_step = std::max(0, knob("LBM_DEBUG_RES_STALL_STEP", 1));
+        res_timeout_ms = std::min(std::max(knob("LBM_DEBUG_RES_TIMEOUT_MS", res_timeout_ms), 1), 60000);
+        res_hog_ms = std::min(std::max(knob("LBM_DEBUG_RES_HOG_MS", 0), 0), 10000);
+        res_hog_wgs = std::max(knob("LBM_DEBUG_RES_HOG_WGS", 0), 0);
         res_per_cu = std::min(std::max(knob("LBM_RES_PER_CU", res_per_cu), 1), 2);
         res_early_poll = knob("LBM_RES_EARLY", res_early_poll) != 0 ? 1 : 0;
         resident_max_cells = std::max(0, knob("LBM_RES_MAX_CELLS", (int)resident_max_cells));
         delay_sub = knob("LBM_DEBUG_DELAY_SUB", -1);
         delay_us = std::min(std::max(knob("LBM_DEBUG_DELAY_US", 0), 0), 100000);
-        no_own_wait = knob("LBM_DEBUG_NO_OWN_WAIT", 0) != 0;
+        // only together with a stall, and never silently: it removes the
+        // round-4 race fix so the ordering test can show the race
+        no_own_wait = delay_sub >= 0 && knob("LBM_DEBUG_NO_OWN_WAIT", 0) != 0;
+        if (no_own_wait)
+            fprintf(stderr, "lbm: LBM_DEBUG_NO_OWN_WAIT=1 -- the loop-back unpack's own-event wait is OFF "
+                            "(debug only: lattices may be wrong)\n");
         if (const char *k = knob_str("LBM_KERNEL")) {
             const std::string v(k);
             env_kernel = v == "pipeline" ? LBM_KERNEL_PIPELINE
@@ -1211,14 +1239,19 @@ struct lbm_handle {
         fill_zero(res_status, 64, s.s_comp);
         int khz = 0;
         HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.dev));
-        res_timeout = (long long)std::max(khz, 1000) * 2000;  // 2 s of wall clock per poll phase
+        res_timeout = (long long)std::max(khz, 1000) * res_timeout_ms;  // 2 s of wall clock per poll phase
         return true;
     }
 
     // Every step of the run in one cooperative launch (lbm_resident.hip),
     // then the fixed-order |u| fold.  The ghost ring of the result is not
-    // maintained (only the resident kernel runs on this handle).
-    void run_resident(int steps, bool accelerate_first) {
+    // maintained (the resident kernel reads the periodic images itself; a
+    // STEP2 fallback rebuilds it).  Returns false when a neighbour hand-off
+    // timed out (the tiles were not all co-resident): the kernel only reads
+    // s.o[s.cur] and writes the other lattice, so the input lattice -- with
+    // the first accelerate applied -- is intact, and s.cur, res_tag and
+    // last_steps are left as they were.
+    bool run_resident(int steps, bool accelerate_first) {
         Sub &s = subs[0];
         set_device(s);
         const int ntiles = res_tx * res_ty;
@@ -1263,6 +1296,8 @@ struct lbm_handle {
             a.status = res_status;
             a.timeout_ticks = res_timeout;
             a.early_poll = res_early_poll;
+            a.stall_tile = res_stall_tile;
+            a.stall_step = res_stall_step;
             long long *trace = nullptr;
             unsigned long long *htrace = nullptr;
             const int trace_steps = std::min(steps, 256);
@@ -1278,6 +1313,15 @@ struct lbm_handle {
                 HIP_CHECK(hipMalloc(&htrace, n));
                 HIP_CHECK(hipMemsetAsync(htrace, 0, n, s.s_comp));
                 a.htrace = htrace;
+            }
+            if (res_hog_ms > 0) {  // debug: hold part of the device's CUs while the grid is dispatched
+                int cus = 0;
+                HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev));
+                if (!res_hog_stream) HIP_CHECK(hipStreamCreateWithFlags(&res_hog_stream, hipStreamNonBlocking));
+                if (!res_hog_sink) HIP_CHECK(hipMalloc(&res_hog_sink, 64));
+                HIP_CHECK(launch_debug_lds_hog(res_hog_ms, res_hog_wgs > 0 ? res_hog_wgs : cus / 2, res_hog_sink,
+                                               res_hog_stream));
+                HIP_CHECK(launch_debug_spin(2000, s.s_comp));  // the hog is dispatched first
             }
             timed(s, s.s_comp, std::string("resident_steps (all steps, one launch)") + (tolerance && RES_VER[res_variant] >= 2 ? " tolerance" : ""),
                   [&] {
@@ -1339,22 +1383,25 @@ struct lbm_handle {
                         "poll %.3f barrier %.3f total %.3f\n", p.nx, p.ny, RES_TH[res_variant], ph[0] * us, ph[1] * us,
                         ph[2] * us, ph[3] * us, ph[4] * us);
             }
-            res_tag += (unsigned)steps;
             timed(s, s.s_comp, "resident_reduce",
                   [&] { HIP_CHECK(launch_resident_reduce(res_partials, s.av_local, steps, ntiles, s.s_comp)); });
-            s.cur ^= 1;
         }
         HIP_CHECK(hipEventRecord(t1, s.s_comp));
         HIP_CHECK(hipEventSynchronize(t1));
+        if (res_hog_stream) HIP_CHECK(hipStreamSynchronize(res_hog_stream));
         float ms = 0.f;
         HIP_CHECK(hipEventElapsedTime(&ms, t0, t1));
         int status = 0;
         HIP_CHECK(hipMemcpy(&status, res_status, sizeof(int), hipMemcpyDeviceToHost));
-        if (status != 0)
-            throw lbm_failure(LBM_E_INTERNAL, "resident kernel: a neighbour hand-off timed out (tiles not co-resident?)");
+        prof_collect();
+        if (status != 0) return false;
+        if (steps > 0) {
+            res_tag += (unsigned)steps;
+            s.cur ^= 1;
+        }
         last_seconds = ms * 1e-3;
         last_steps = steps;
-        prof_collect();
+        return true;
     }
 
     // Unfused pipeline, one kernel per stage (lbm_pipeline.hip): every step
@@ -1882,9 +1929,23 @@ struct lbm_handle {
         run_fused = run_single = 0;
         prof_drop();
         if (resident) {
-            run_resident(steps, accelerate_first);
-            run_fused = steps > 0 ? 1 : 0;
-            return;
+            if (run_resident(steps, accelerate_first)) {
+                run_fused = steps > 0 ? 1 : 0;
+                return;
+            }
+            // Residency failure (another kernel held CUs, so part of the grid
+            // waited behind tiles that waited for it): repeat the run on the
+            // STEP2 kernel from the intact input lattice, which already
+            // carries the run's first accelerate, and stay on STEP2 -- the
+            // blocking engine.run(1) contract of LbmRunner.cpp:102-104 holds
+            // whatever else runs on the device.
+            resident = false;
+            res_failed = true;
+            ring_stale = true;  // the resident kernel kept no ghost ring
+            accelerate_first = false;
+            fprintf(stderr, "lbm: resident kernel hand-off timed out (tiles not co-resident); "
+                            "run repeated on the step2 kernel, which this handle keeps from now on\n");
+            prof_drop();
         }
         if (pipeline) {
             run_pipeline(steps);
@@ -2150,6 +2211,8 @@ struct lbm_handle {
             if (s.ev_u) (void)hipEventDestroy(s.ev_u);
             if (s.ev_end) (void)hipEventDestroy(s.ev_end);
         }
+        if (res_hog_stream) (void)hipStreamDestroy(res_hog_stream);
+        if (res_hog_sink) (void)hipFree(res_hog_sink);
         if (res_halo) (void)hipFree(res_halo);
         if (res_partials) (void)hipFree(res_partials);
         if (res_status) (void)hipFree(res_status);

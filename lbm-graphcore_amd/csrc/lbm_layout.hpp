@@ -222,6 +222,10 @@ struct ResidentArgs {
     int trace_steps;
     unsigned long long *htrace;  // LBM_RES_TRACE=2: [step][tile][2] latest wave's collision end, ring ready
     int early_poll;         // v2: poll the ring after the first work item instead of after the last
+    // LBM_DEBUG_RES_STALL_TILE / _STEP (debug knobs, tests/test_gpu_resident_recovery.py):
+    // tile stall_tile leaves the step loop at step stall_step without publishing,
+    // as a tile that never became resident would -- a deterministic residency failure
+    int stall_tile, stall_step;
 };
 
 // Halo pack (edge -> dst) after load / accelerate, and unpack (recv -> ghost

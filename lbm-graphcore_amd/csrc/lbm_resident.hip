@@ -62,11 +62,14 @@ __device__ __forceinline__ float rdlane(float v, int l) {
 // cg on lanes that pass one.  Every round issues all outstanding loads back
 // to back (one memory round trip per round, not one per granule) and
 // re-polls only the granules whose tag is not there yet.  v[j * 3 + i] /
-// v[3 * NPOS] receive the values; false on deadline.
+// v[3 * NPOS] receive the values; false on deadline, or as soon as another tile
+// has reported a timeout in *status (the whole grid then drains within one
+// poll round instead of one deadline per ring of neighbours).
 
 template <int NPOS>
 __device__ __forceinline__ bool fetch_ring(const unsigned long long *g, int len, const unsigned long long *cg,
-                                           unsigned tag, long long deadline, float (&v)[3 * NPOS + 1]) {
+                                           unsigned tag, long long deadline, const int *status,
+                                           float (&v)[3 * NPOS + 1]) {
     constexpr int N = 3 * NPOS + 1;
     const int lane = threadIdx.x & 63;
     unsigned pending = 0;
@@ -92,6 +95,7 @@ __device__ __forceinline__ bool fetch_ring(const unsigned long long *g, int len,
             }
         if (!pending) return true;
         if ((long long)wall_clock64() > deadline) return false;
+        if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -164,6 +168,7 @@ __global__ __launch_bounds__(64 * NW) void resident_steps(ResidentArgs a) {
     const long long deadline_span = a.timeout_ticks;
     int t = 0;
     for (; t < a.steps; ++t) {
+        if (tile == a.stall_tile && t == a.stall_step) break;  // debug: a tile that stops publishing
         const bool tr = a.trace && tile == 0 && threadIdx.x == 0 && t < a.trace_steps;
         if (tr) a.trace[t * 5 + 0] = (long long)wall_clock64();
         if (t > 0 && threadIdx.x == 0) {
@@ -263,7 +268,7 @@ __global__ __launch_bounds__(64 * NW) void resident_steps(ResidentArgs a) {
             const unsigned long long *cg =
                 corner ? gbase(slot, (side == 0 ? tys : tyn) * a.tiles_x + (left ? txw : txe), cd) : nullptr;
             float v[4];
-            ok = ok && fetch_ring<1>(gbase(slot, src_tile, d), len, cg, tag, deadline, v);
+            ok = ok && fetch_ring<1>(gbase(slot, src_tile, d), len, cg, tag, deadline, a.status, v);
             const int p = lane;
             if (p < len) {
                 const int lx = side < 2 ? p : (side == 2 ? -1 : tw);
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
                 const unsigned long long *cg =
                     corner ? gbase(slot, (side == 0 ? tys : tyn) * a.tiles_x + (left ? txw : txe), cd) : nullptr;
                 float v[7];
-                ok = ok && fetch_ring<2>(gbase(slot, src_tile, d), len, cg, tag, deadline, v);
+                ok = ok && fetch_ring<2>(gbase(slot, src_tile, d), len, cg, tag, deadline, a.status, v);
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int p = lane + 64 * j;
@@ -571,6 +576,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void resident_steps2(ResidentArgs a)
         return !abort_flag;
     };
     for (; t < a.steps; ++t) {
+        if (tile == a.stall_tile && t == a.stall_step) break;  // debug: a tile that stops publishing
         if (!step()) break;
     }
     if (t == a.steps && a.steps > 0 && threadIdx.x == 0) {
@@ -653,12 +659,13 @@ hipError_t resident_capacity(int variant, int device, bool tol, int &capacity) {
     return hipSuccess;
 }
 
-// coop: hipLaunchCooperativeKernel (the runtime rejects a grid that cannot be
-// fully resident; HIP runs it on its own cooperative queue); else a plain
-// launch of a grid the engine has already sized to the occupancy capacity
-// (resident_capacity), co-resident on an otherwise idle device -- and if it
-// ever is not, the kernel's 2 s poll deadline drains the grid and the run
-// reports LBM_E_INTERNAL instead of hanging.
+// coop (default): hipLaunchCooperativeKernel (the runtime rejects a grid that
+// cannot be fully resident; HIP runs it on its own cooperative queue); else a
+// plain launch of a grid the engine has already sized to the occupancy
+// capacity (resident_capacity).  Neither makes the tiles co-resident when
+// another kernel holds CUs: then the poll deadline drains the grid, the
+// engine finds the status word set and repeats the run on the STEP2 kernel
+// from the untouched input lattice (lbm_engine.hip run_steps).
 hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, bool coop, hipStream_t s) {
     int threads = 0;
     const void *fn = resident_kernel(variant, threads, tol);
@@ -666,6 +673,25 @@ hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, bool co
     void *params[] = {&arg};
     if (coop) return hipLaunchCooperativeKernel(fn, dim3(a.tiles_x * a.tiles_y), dim3(threads), params, 0, s);
     return hipLaunchKernel(fn, dim3(a.tiles_x * a.tiles_y), dim3(threads), params, 0, s);
+}
+
+// Debug (LBM_DEBUG_RES_HOG_MS / _WGS): one-wave workgroups that each hold
+// 152 KiB of LDS -- a whole CU for any resident tile -- for `ticks` of wall
+// clock, launched on another stream just before the resident grid, so that
+// only part of the grid can become resident: a real co-residency failure.
+__global__ __launch_bounds__(64) void debug_lds_hog(long long ticks, float *sink) {
+    __shared__ float hold[38912];  // 152 KiB
+    const long long end = (long long)wall_clock64() + ticks;
+    hold[threadIdx.x * 600] = (float)threadIdx.x;
+    while ((long long)wall_clock64() < end) __builtin_amdgcn_s_sleep(8);
+    __syncthreads();
+    if (threadIdx.x == 0 && hold[600] == -1.f) sink[0] = hold[1200];  // never true: keeps the allocation
+}
+
+hipError_t launch_debug_lds_hog(int milliseconds, int workgroups, float *sink, hipStream_t s) {
+    if (milliseconds <= 0 || workgroups <= 0) return hipSuccess;
+    hipLaunchKernelGGL(debug_lds_hog, dim3(workgroups), dim3(64), 0, s, (long long)milliseconds * 100000, sink);
+    return hipGetLastError();
 }
 
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s) {

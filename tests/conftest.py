@@ -26,9 +26,10 @@ for p in (str(ROOT), str(PKG)):
 from lbm_amd import io as lio  # noqa: E402
 
 # The library reads its tuning knobs (LBM_STREAM_CFG, LBM_TILE2, ...) only with
-# LBM_DEBUG_KNOBS=1; the tests that select variants through them need it.
-# Unset knobs keep the product defaults.
-os.environ.setdefault("LBM_DEBUG_KNOBS", "1")
+# LBM_DEBUG_KNOBS=1.  No session-wide default: the test modules that select
+# variants through knobs opt in with the `debug_knobs` fixture (per test,
+# undone after it), and tests/test_gpu_product_mode.py checks that a handle
+# created without the gate ignores stray knobs.
 
 GRIDS = ["128x128", "128x256", "256x256", "1024x1024"]
 
@@ -106,6 +107,12 @@ def small_problems():
         out[name] = (p, data[f"{name}/obstacles"], data[f"{name}/cells0"],
                      {n: (data[f"{name}/cells_after_{n}"], data[f"{name}/av_{n}"]) for n in (1, 2, 10)})
     return out
+
+
+@pytest.fixture
+def debug_knobs(monkeypatch):
+    """LBM_DEBUG_KNOBS=1 for one test: the library then reads its tuning / debug knobs."""
+    monkeypatch.setenv("LBM_DEBUG_KNOBS", "1")
 
 
 @pytest.fixture(scope="session")

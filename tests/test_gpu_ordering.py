@@ -27,7 +27,7 @@ from conftest import load_problem
 from lbm_amd import io as lio
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("debug_knobs")]  # tests select variants by knob
 
 STALL_US = "3000"   # per stalled launch; a 128x256 step of a neighbour takes ~10 us
 

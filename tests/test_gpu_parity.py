@@ -19,7 +19,7 @@ from conftest import GOLD, GRIDS, check_gate, load_problem, oracle_av_vels, orac
 from lbm_amd import io as lio
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("debug_knobs")]  # tests select variants by knob
 
 # av_vels: per-step sum of |u| over up to 1M cells in fp32; the oracle adds
 # sequentially, the GPU in fixed-order trees.  Observed differences are far

@@ -27,7 +27,7 @@ from conftest import GRIDS, check_gate, load_problem, oracle_av_vels, oracle_man
 from lbm_amd import io as lio
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("debug_knobs")]  # tests select variants by knob
 
 TOL_POP = 2e-5   # max |f_gpu - f_oracle| / |f_oracle| over every population (<= 100 steps)
 TOL_AV = 2e-4    # av_vels, relative
@@ -39,7 +39,7 @@ TOL_AV = 2e-4    # av_vels, relative
 # Newton step: profiles/r05/final_prev/pytest_tol.log; round 5 with it: 4.3e-4
 # .. 8.5e-4 and 2.4e-4 .. 8.7e-4, profiles/r05/gate/).
 TOL_POP_FULL = 2e-3
-TOL_AV_FULL = 3e-3
+TOL_AV_FULL = 2e-3  # measured <= 1.5e-3 (profiles/r05/gate/)
 
 
 @functools.lru_cache(maxsize=4)

@@ -21,7 +21,7 @@ from lbm_amd import io as lio
 from oracle import oracle
 import test_d3q19 as T3
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("debug_knobs")]  # tests select variants by knob
 
 
 @pytest.fixture(autouse=True)
