@@ -477,7 +477,12 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
     n3 = steps // 3 * 3 if three else 0
     n2 = (steps - n3) // 2 * 2 if two else 0
     alg_b = (n3 * b3 + n2 * b2 + (steps - n3 - n2) * 152) / max(steps, 1)
+    # compulsory bytes: each pass moves the lattice through HBM once, 152 B
+    # per cell per pass -- 152 / S per update for S steps per pass, without
+    # the blocks' overlap re-reads (which b2 / b3 count as algorithmic)
+    comp_b = (n3 * 152 / 3 + n2 * 152 / 2 + (steps - n3 - n2) * 152) / max(steps, 1)
     per_gpu_gbs = alg_b * cells / world * steps / dev / 1e9
+    comp_gbs = comp_b * cells / world * steps / dev / 1e9
     return {"grid": f"{n}^3", "steps": steps, "settle_steps": nset, "decomposition": f"{world} z slabs",
             "numerics": "tolerance" if flags & native.FLAG_TOLERANCE else "bitwise",
             "kernel": (f"step3d_three ({n3 // 3} passes of 3 steps) + step3d_two ({n2 // 2} of 2)" if three else
@@ -485,9 +490,13 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
             "av_vels_finite": finite, "mlups": round(cells * steps / secs / 1e6, 1) if finite else None,
             "ms_per_step": round(secs / steps * 1e3, 4),
             "hbm_gbs_per_gpu": round(per_gpu_gbs, 1), "hbm_frac": round(per_gpu_gbs / HBM_PEAK_GBS, 4),
+            "compulsory_b_per_update": round(comp_b, 2),
+            "hbm_gbs_compulsory_per_gpu": round(comp_gbs, 1),
+            "hbm_frac_compulsory": round(comp_gbs / HBM_PEAK_GBS, 4),
             "effective_gbs_per_gpu": round(152 * cells / world * steps / dev / 1e9, 1),
-            "note": f"{alg_b:.1f} algorithmic B per update, mean over the passes (152 = 19 fp32 loads + stores per step; effective_gbs on "
-                    "that basis); parity unpinned upstream (no 3-D reference)"}
+            "note": f"hbm_frac: {alg_b:.1f} B per update including the blocks' overlap re-reads; hbm_frac_compulsory: "
+                    f"{comp_b:.1f} B per update, the lattice once per pass (152 B = 19 fp32 loads + stores per cell; "
+                    "effective_gbs on that basis per step); parity unpinned upstream (no 3-D reference)"}
 
 
 def _check_cases(world: int):

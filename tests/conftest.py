@@ -19,6 +19,7 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "lbm-graphcore_amd"
 GOLD = ROOT / "tests" / "golden"
+TESTS_DIR = ROOT / "tests"
 for p in (str(ROOT), str(PKG)):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -117,13 +117,13 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run(inject: str, timeout: float = 120):
+def _run(inject: str, timeout: float = 120, world: int = 2):
     code = WORKER.format(root=str(ROOT), pkg=str(PKG))
     port = _free_port()
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), INJECT=inject)
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), INJECT=inject, OMP_NUM_THREADS="1")
         procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     out = []
@@ -170,3 +170,25 @@ def test_failed_check_is_fatal_on_every_rank(inject, rank_failed):
     if inject.startswith("raise"):
         assert "injected" in cases["b"]["errors"][str(rank_failed)]  # JSON object keys are strings
     assert not [ln for ln in out[1][1].splitlines() if ln.startswith("{")]  # only rank 0 prints the line
+
+
+@pytest.mark.parametrize("inject,rank_failed", [("", None), ("corrupt_rank1", 1), ("raise_run_rank1", 1)])
+def test_check_gate_at_eight_ranks(inject, rank_failed):
+    """The driver's 8-GPU node: the same gate with a world of 8 (reference rule
+    2x4, 8x1 and 1x8 cases) -- one failing rank stops all eight before timing."""
+    out = _run(inject, world=8)
+    if rank_failed is None:
+        for rc, o, e in out:
+            assert rc == 0, e
+            assert "PASSED_GATE" in o
+        return
+    for rc, o, e in out:
+        assert rc == _bench_const("CHECK_FAILED_EXIT"), e
+        assert "PASSED_GATE" not in o
+    lines = [ln for ln in out[0][1].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[0][1]
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["n_gpus"] == 8
+    assert d["multi_rank_check"]["cases"]["b"]["ranks_failed"] == [rank_failed]
+    for r in range(1, 8):
+        assert not [ln for ln in out[r][1].splitlines() if ln.startswith("{")]

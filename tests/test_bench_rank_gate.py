@@ -1,4 +1,4 @@
-"""bench.py's _RankGate (CPU, gloo world of 2): when one rank raises inside a
+"""bench.py's _RankGate (CPU, gloo worlds of 2 and 8): when one rank raises inside a
 host-side phase of a multi-rank aux measurement, EVERY rank raises at the
 same gate -- nobody is left blocked in the next collective -- and the engine
 that rank holds is closed.  Stand-in engines: the control flow is under test,
@@ -66,15 +66,17 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("stage,fail_rank", [("setup", 1), ("timed", 0), ("timed", 1), ("none", 0)])
-def test_rank_gate_all_ranks_raise_together(tmp_path, stage, fail_rank):
+@pytest.mark.parametrize("world,stage,fail_rank", [(2, "setup", 1), (2, "timed", 0), (2, "timed", 1), (2, "none", 0),
+                                                    # the driver's 8-GPU node: one rank of eight fails
+                                                    (8, "setup", 5), (8, "timed", 7), (8, "none", 0)])
+def test_rank_gate_all_ranks_raise_together(tmp_path, world, stage, fail_rank):
     script = tmp_path / "w.py"
     script.write_text(WORKER.format(root=str(ROOT), pkg=str(PKG)))
     port = _free_port()
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   FAIL_STAGE=stage, FAIL_RANK=str(fail_rank))
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   FAIL_STAGE=stage, FAIL_RANK=str(fail_rank), OMP_NUM_THREADS="1")
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=120) for p in procs]
