@@ -62,7 +62,16 @@ enum { LBM_TRANSPORT_LOCAL = 0, LBM_TRANSPORT_RCCL = 1 };
  * steps (else K % S one-step launches), single and decomposed domains alike.  RESIDENT: every step of a run in one persistent
  * launch with the lattice held on chip (LDS + registers) -- single
  * sub-domain grids small enough for all of their 64-column tiles to be
- * co-resident (1024x1024 and below on MI355X).  PIPELINE: the unfused
+ * co-resident (1024x1024 and below on MI355X).  Its tiles hand populations to
+ * each other through device memory, so all of them must run at once: the
+ * grid is sized to the device's occupancy and launched cooperatively; if it
+ * still cannot become co-resident (another kernel holding CUs: the runtime
+ * refuses the cooperative launch, or a neighbour hand-off passes its 2 s
+ * deadline) the run is repeated on the STEP2 kernel from the run's input
+ * lattice -- untouched by the failed launch -- and returns LBM_OK with the
+ * same lattice and av_vels; the handle keeps STEP2 afterwards
+ * (lbm_kernel_in_use reports it, lbm_numerics reports bitwise) and prints one
+ * line to stderr.  No run waits longer than one deadline for this.  PIPELINE: the unfused
  * reference pipeline, one kernel per stage and step (accelerate_flow ->
  * propagate -> rebound -> textbook BGK collision -> av_velocity,
  * main/LbmPoplibs.cpp:225-233) with the conditional accelerate at the start

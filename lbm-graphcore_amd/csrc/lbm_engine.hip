@@ -70,7 +70,6 @@ hipError_t launch_pipe_av(const float *partials, int n, float *av_local, int t, 
 hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, bool coop, hipStream_t s);
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s);
 hipError_t launch_debug_spin(int microseconds, hipStream_t s);
-hipError_t launch_debug_lds_hog(int milliseconds, int workgroups, float *sink, hipStream_t s);
 }  // namespace lbm
 
 using namespace lbm;
@@ -265,9 +264,7 @@ struct lbm_handle {
     bool res_failed = false;        // a resident run timed out: this handle runs STEP2 from then on
     int res_stall_tile = -1, res_stall_step = 1;  // LBM_DEBUG_RES_STALL_TILE / _STEP
     int res_timeout_ms = 2000;      // LBM_DEBUG_RES_TIMEOUT_MS: poll deadline
-    int res_hog_ms = 0, res_hog_wgs = 0;  // LBM_DEBUG_RES_HOG_MS / _WGS: LDS hog beside the launch
-    hipStream_t res_hog_stream = nullptr;
-    float *res_hog_sink = nullptr;
+    bool res_oversubscribe = false; // LBM_DEBUG_RES_OVERSUBSCRIBE: skip the capacity check of the tile choice
     int res_tx = 0, res_ty = 0;
     unsigned long long *res_halo = nullptr;
     float *res_partials = nullptr;
@@ -478,8 +475,7 @@ struct lbm_handle {
         res_stall_tile = knob("LBM_DEBUG_RES_STALL_TILE", -1);
         res_stall_step = std::max(0, knob("LBM_DEBUG_RES_STALL_STEP", 1));
         res_timeout_ms = std::min(std::max(knob("LBM_DEBUG_RES_TIMEOUT_MS", res_timeout_ms), 1), 60000);
-        res_hog_ms = std::min(std::max(knob("LBM_DEBUG_RES_HOG_MS", 0), 0), 10000);
-        res_hog_wgs = std::max(knob("LBM_DEBUG_RES_HOG_WGS", 0), 0);
+        res_oversubscribe = knob("LBM_DEBUG_RES_OVERSUBSCRIBE", 0) != 0;
         res_per_cu = std::min(std::max(knob("LBM_RES_PER_CU", res_per_cu), 1), 2);
         res_early_poll = knob("LBM_RES_EARLY", res_early_poll) != 0 ? 1 : 0;
         resident_max_cells = std::max(0, knob("LBM_RES_MAX_CELLS", (int)resident_max_cells));
@@ -1222,7 +1218,9 @@ struct lbm_handle {
             int cap = 0;
             HIP_CHECK(resident_capacity(v, s.dev, tolerance && RES_VER[v] >= 2, cap));
             const long long n = (long long)tx * ty;
-            if (n <= cap && n <= (long long)res_per_cu * cus) {
+            // LBM_DEBUG_RES_OVERSUBSCRIBE=1: take the first tile shape whatever
+            // the capacity -- a grid that cannot be co-resident (tests)
+            if ((n <= cap && n <= (long long)res_per_cu * cus) || res_oversubscribe) {
                 res_variant = v;
                 res_tx = tx;
                 res_ty = ty;
@@ -1314,20 +1312,19 @@ struct lbm_handle {
                 HIP_CHECK(hipMemsetAsync(htrace, 0, n, s.s_comp));
                 a.htrace = htrace;
             }
-            if (res_hog_ms > 0) {  // debug: hold part of the device's CUs while the grid is dispatched
-                int cus = 0;
-                HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev));
-                if (!res_hog_stream) HIP_CHECK(hipStreamCreateWithFlags(&res_hog_stream, hipStreamNonBlocking));
-                if (!res_hog_sink) HIP_CHECK(hipMalloc(&res_hog_sink, 64));
-                HIP_CHECK(launch_debug_lds_hog(res_hog_ms, res_hog_wgs > 0 ? res_hog_wgs : cus / 2, res_hog_sink,
-                                               res_hog_stream));
-                HIP_CHECK(launch_debug_spin(2000, s.s_comp));  // the hog is dispatched first
-            }
+            bool rejected = false;  // the cooperative launch refused the grid: a residency failure too
             timed(s, s.s_comp, std::string("resident_steps (all steps, one launch)") + (tolerance && RES_VER[res_variant] >= 2 ? " tolerance" : ""),
                   [&] {
-                      HIP_CHECK(launch_resident(a, res_variant, tolerance && RES_VER[res_variant] >= 2, res_coop,
-                                                s.s_comp));
+                      const hipError_t e = launch_resident(a, res_variant, tolerance && RES_VER[res_variant] >= 2,
+                                                           res_coop, s.s_comp);
+                      if (e == hipErrorCooperativeLaunchTooLarge) {
+                          (void)hipGetLastError();
+                          rejected = true;
+                      } else {
+                          HIP_CHECK(e);
+                      }
                   });
+            if (rejected) HIP_CHECK(hipMemsetAsync(res_status, 0xff, sizeof(int), s.s_comp));
             if (htrace) {  // per tile and step: wait for the slowest neighbour, then the hop itself
                 std::vector<unsigned long long> hv((size_t)2 * trace_steps * ntiles);
                 HIP_CHECK(hipMemcpyAsync(hv.data(), htrace, hv.size() * 8, hipMemcpyDeviceToHost, s.s_comp));
@@ -1388,7 +1385,6 @@ struct lbm_handle {
         }
         HIP_CHECK(hipEventRecord(t1, s.s_comp));
         HIP_CHECK(hipEventSynchronize(t1));
-        if (res_hog_stream) HIP_CHECK(hipStreamSynchronize(res_hog_stream));
         float ms = 0.f;
         HIP_CHECK(hipEventElapsedTime(&ms, t0, t1));
         int status = 0;
@@ -2211,8 +2207,6 @@ struct lbm_handle {
             if (s.ev_u) (void)hipEventDestroy(s.ev_u);
             if (s.ev_end) (void)hipEventDestroy(s.ev_end);
         }
-        if (res_hog_stream) (void)hipStreamDestroy(res_hog_stream);
-        if (res_hog_sink) (void)hipFree(res_hog_sink);
         if (res_halo) (void)hipFree(res_halo);
         if (res_partials) (void)hipFree(res_partials);
         if (res_status) (void)hipFree(res_status);

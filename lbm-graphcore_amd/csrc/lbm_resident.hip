@@ -675,25 +675,6 @@ hipError_t launch_resident(const ResidentArgs &a, int variant, bool tol, bool co
     return hipLaunchKernel(fn, dim3(a.tiles_x * a.tiles_y), dim3(threads), params, 0, s);
 }
 
-// Debug (LBM_DEBUG_RES_HOG_MS / _WGS): one-wave workgroups that each hold
-// 152 KiB of LDS -- a whole CU for any resident tile -- for `ticks` of wall
-// clock, launched on another stream just before the resident grid, so that
-// only part of the grid can become resident: a real co-residency failure.
-__global__ __launch_bounds__(64) void debug_lds_hog(long long ticks, float *sink) {
-    __shared__ float hold[38912];  // 152 KiB
-    const long long end = (long long)wall_clock64() + ticks;
-    hold[threadIdx.x * 600] = (float)threadIdx.x;
-    while ((long long)wall_clock64() < end) __builtin_amdgcn_s_sleep(8);
-    __syncthreads();
-    if (threadIdx.x == 0 && hold[600] == -1.f) sink[0] = hold[1200];  // never true: keeps the allocation
-}
-
-hipError_t launch_debug_lds_hog(int milliseconds, int workgroups, float *sink, hipStream_t s) {
-    if (milliseconds <= 0 || workgroups <= 0) return hipSuccess;
-    hipLaunchKernelGGL(debug_lds_hog, dim3(workgroups), dim3(64), 0, s, (long long)milliseconds * 100000, sink);
-    return hipGetLastError();
-}
-
 hipError_t launch_resident_reduce(const float *partials, float *av_local, int steps, int ntiles, hipStream_t s) {
     if (steps <= 0) return hipSuccess;
     hipLaunchKernelGGL(resident_reduce, dim3((steps + 3) / 4), dim3(256), 0, s, partials, av_local, steps, ntiles);

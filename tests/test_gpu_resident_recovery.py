@@ -12,11 +12,11 @@ lbm_run keeps the blocking engine.run(1) contract of the reference host
 Failure injection (debug knobs, read only with LBM_DEBUG_KNOBS=1):
   * LBM_DEBUG_RES_STALL_TILE / _STEP: one tile leaves its step loop without
     publishing -- a residency failure on every launch mode, every time;
-  * LBM_DEBUG_RES_HOG_MS / _WGS: a kernel on another stream holds 152 KiB of
-    LDS on half of the CUs while the grid is dispatched -- a real co-residency
-    failure for the plain launch (what the cooperative launch does is recorded);
+  * LBM_DEBUG_RES_OVERSUBSCRIBE: a grid with more tiles than the device holds
+    (the cooperative launch is refused, the plain one times out);
   * LBM_DEBUG_RES_TIMEOUT_MS shortens the 2 s poll deadline.
-Every result is compared bitwise with the CPU oracle.
+And without injection: the reference run beside another handle that keeps the
+device busy.  Every result is compared bitwise with the CPU oracle.
 """
 from __future__ import annotations
 
@@ -32,6 +32,10 @@ from lbm_amd import io as lio
 from oracle import oracle
 
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("debug_knobs")]
+
+# av_vels: the oracle sums |u| of 262 144 cells sequentially in fp32, the GPU in
+# fixed-order trees (the lattices are compared bitwise)
+AV_RTOL = 1e-4
 
 
 def sha(cells):
@@ -76,10 +80,10 @@ def test_stalled_tile_falls_back_bitwise(gpu_lib, coop, flags, monkeypatch):
         c2, av2 = e.store(n_av=steps2)
     ref1, ref_av1 = oracle.run(p, obst, steps1, cells0)
     assert np.array_equal(c1, ref1)
-    np.testing.assert_allclose(av1, ref_av1, rtol=1e-5)
+    np.testing.assert_allclose(av1, ref_av1, rtol=AV_RTOL)
     ref2, ref_av2 = oracle.run(p, obst, steps2, ref1, accelerate_first=False)
     assert np.array_equal(c2, ref2)
-    np.testing.assert_allclose(av2, ref_av2, rtol=1e-5)
+    np.testing.assert_allclose(av2, ref_av2, rtol=AV_RTOL)
 
 
 def test_stall_without_knob_gate_is_ignored(gpu_lib, monkeypatch):
@@ -97,33 +101,32 @@ def test_stall_without_knob_gate_is_ignored(gpu_lib, monkeypatch):
     assert np.array_equal(cells, ref)
 
 
-@pytest.mark.parametrize("coop", ["0", "1"])
-def test_lds_hog_on_half_the_cus(gpu_lib, coop, monkeypatch, capfd):
-    """A kernel holding half of the CUs (152 KiB of LDS each, 300 ms) while the
-    resident grid is dispatched: the run ends bitwise equal to the oracle on
-    whichever kernel finished it.  The plain launch cannot become co-resident
-    and must fall back; the cooperative launch's outcome is recorded."""
+@pytest.mark.parametrize("coop", ["1", "0"])
+def test_oversubscribed_grid_falls_back(gpu_lib, coop, monkeypatch, capfd):
+    """A resident grid larger than the device holds at once (1024^2 in 128x4
+    tiles: 2048 workgroups, about three per CU fit): the cooperative launch is
+    refused by the runtime, the plain launch's resident part times out while
+    the rest waits -- both end on STEP2 with the oracle's lattice."""
     monkeypatch.setenv("LBM_RES_COOP", coop)
-    monkeypatch.setenv("LBM_DEBUG_RES_HOG_MS", "300")
+    monkeypatch.setenv("LBM_DEBUG_RES_OVERSUBSCRIBE", "1")
+    monkeypatch.setenv("LBM_RES_TH", "4")
     monkeypatch.setenv("LBM_DEBUG_RES_TIMEOUT_MS", "100")
-    p, obst, cells0 = _problem()
-    steps = 60
+    p, obst = load_problem("1024x1024", iters=30)
+    cells0 = lio.init_cells(p)
     with gpu_lib.Engine(p, obst) as e:
         assert e.kernel_in_use() == "resident"
         e.load_cells(cells0)
         t0 = time.monotonic()
-        e.run_steps(steps, accelerate_first=True)
+        e.run()
         wall = time.monotonic() - t0
-        used = e.kernel_in_use()
-        cells, av = e.store(n_av=steps)
-    err = capfd.readouterr().err
-    print(f"coop={coop}: finished on {used} in {wall:.3f} s")
+        assert e.kernel_in_use() == "step2"
+        cells, av = e.store()
+    assert "hand-off timed out" in capfd.readouterr().err
+    print(f"coop={coop}: oversubscribed grid fell back to step2 in {wall:.3f} s")
     assert wall < 10.0
-    if coop == "0":
-        assert used == "step2" and "hand-off timed out" in err
-    ref, ref_av = oracle.run(p, obst, steps, cells0)
+    ref, ref_av = oracle.run(p, obst, 30, cells0)
     assert np.array_equal(cells, ref)
-    np.testing.assert_allclose(av, ref_av, rtol=1e-5)
+    np.testing.assert_allclose(av, ref_av, rtol=AV_RTOL)
 
 
 def test_reference_run_beside_a_busy_handle(gpu_lib):
