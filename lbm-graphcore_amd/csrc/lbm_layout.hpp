@@ -174,7 +174,6 @@ struct StreamArgs {
     float *av_local;
     int *ctl;
     int n_total, stride;
-    int mirror;             // LBM_STREAM_MIRROR (A/B): odd segments walk their rows bottom-up (MIR launch forms)
 };
 
 // Lattice-resident persistent kernel (lbm_resident.hip): tiles of RES_TW

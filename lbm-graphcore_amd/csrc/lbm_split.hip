@@ -156,7 +156,6 @@ void lbm_handle::build_args(Sub &s) {
     b3.w1 = w1;
     b3.w2 = w2;
     b3.ctl = s.ctl;
-    b3.mirror = knob("LBM_STREAM_MIRROR", 0) != 0 ? 1 : 0;
     StreamArgs si = b3, sb = b3;
     s.n3_int = s.n3_bnd = 0;
     if (use_stream) {

@@ -128,17 +128,16 @@ struct Stream2Geo {
     long long P;
     int pitch, xa, xb, yo0, yo1, j0, jlast;
     bool owna, ownb;
-    bool up;  // mirrored walk (odd segment of a MIR launch): rows jlast .. j0, bottom-up
 };
 
 // Prefetch distance PD: the loads of row j+PD (clamped to the segment) are
 // issued while row j is computed -- PD = 2 keeps two rows of every wave in
 // flight (the kernel is bound by the memory-level parallelism of two waves
 // per SIMD, not by VALU: tools/pmc_summary.py SQ_WAIT_ANY), at 18 more VGPRs.
-template <int PD, bool OBST, bool UP = false>
+template <int PD, bool OBST>
 __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2Geo &g, int j, f2 (&v)[Q],
                                               unsigned (&ob)[2]) {
-    const int jn = UP ? max(j, g.j0) : min(j, g.jlast);
+    const int jn = min(j, g.jlast);
     const float *cn = g.src + (long long)jn * g.pitch;
 #pragma unroll
     for (int k = 0; k < Q; ++k) v[k] = *reinterpret_cast<const f2 *>(cn + k * g.P);
@@ -160,17 +159,9 @@ __device__ __forceinline__ void stream2d_load(const StreamArgs &a, const Stream2
 // order) -- 6 VGPRs fewer per level.  (Rounds 3-4 kept the per-level |u|
 // sums there too, S VGPRs fewer; once the in-place shifts freed 32 VGPRs,
 // registers ran the S = 10 launch 2.5 % faster, profiles/r05/swap/us2_*.)
-// UP (LP forms only): the mirrored walk of a segment, rows jlast .. j0 -- level
-// L computes row j + L, the newest level-(L-1) row is y - 1 and the older one
-// y + 1, so planes 4, 7, 8 take the two-deep delay line (registers + LDS
-// slot) that 2, 5, 6 take walking down, and 2, 5, 6 come from the newest row.
-// Neighbouring segments then read their shared 2S boundary rows at the same
-// time (both start, or both end, there) instead of ~a segment's walk apart.
-template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL, bool LP, bool UP = false>
+template <int S, int PAR, bool GUARD, int PD, bool NT, bool OBST, bool TOL, bool LP>
 __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st, int j,
                                              const TolK &tk, f2 *lpl) {
-    static_assert(!UP || (LP && PD == 1), "the mirrored walk exists for the LP forms");
-    constexpr int D = UP ? -1 : 1;  // row step of the walk
     // PD = 1: row j+1 into the other parity's buffer; PD = 2: row j+2 into this one once it is read
     // (LP forms issue row j+1's loads later, at level 2: see below)
     if (PD == 1 && !LP) stream2d_load<PD, OBST>(a, g, j + 1, st.v[1 - PAR], st.ob[1 - PAR]);
@@ -192,25 +183,19 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
 #pragma unroll
     for (int L = 1; L <= S; ++L) {
         const int b = L - 1;
-        const int y = j - D * L;
+        const int y = j - L;
         if constexpr (LP && PD == 1) {
             // LP forms: row j+1 is loaded once level 1 has consumed row j, into
             // the row buffer itself (cur holds row j by then) -- one 18-VGPR
             // row buffer; levels 2..S (>= 5 levels) cover the latency
             if (L == 2) {
-                stream2d_load<PD, OBST, UP>(a, g, j + D, st.v[0], st.ob[0]);
+                stream2d_load<PD, OBST>(a, g, j + 1, st.v[0], st.ob[0]);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
         // pulled populations of row y (level L-1 values; x +- 1 by DPP)
         f2 s[Q];
-        if constexpr (LP && UP) {
-            // mirrored: the registers hold row y+1 of planes 4, 7, 8 (st.p2 /
-            // p5 / p6 hold planes 4 / 7 / 8 here), the LDS slot row y
-            s[4] = st.p2[0][b];
-            s[7] = kept(st.p5[0][b]);
-            s[8] = kept(st.p6[0][b]);
-        } else if constexpr (LP) {
+        if constexpr (LP) {
             // LP: the registers hold row y-1 of planes 2, 5, 6 (the older row),
             // the LDS slot row y; both move on after the collision (below)
             s[2] = st.p2[0][b];
@@ -227,15 +212,9 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         s[0] = st.c0[b];
         s[1] = kept(st.c1[b]);
         s[3] = kept(st.c3[b]);
-        if constexpr (UP) {
-            s[2] = cur[2];
-            s[5] = kept(shl_kept(cur[5]));
-            s[6] = kept(shr_kept(cur[6]));
-        } else {
-            s[4] = cur[4];
-            s[7] = kept(shr_kept(cur[7]));
-            s[8] = kept(shl_kept(cur[8]));
-        }
+        s[4] = cur[4];
+        s[7] = kept(shr_kept(cur[7]));
+        s[8] = kept(shl_kept(cur[8]));
         if constexpr (!LP) {
             st.c0[b] = cur[0];
             st.c1[b] = shl_kept(cur[1]);
@@ -247,7 +226,7 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
         // whole level makes the compiler hold a second copy of the level state
         // in the tolerance forms (S = 7: 234 vs 202 VGPRs, S = 10: 35 spilled
         // vs 254)
-        const bool cold = GUARD && (UP ? j > g.jlast - 2 * L : j < g.j0 + 2 * L);
+        const bool cold = GUARD && j < g.j0 + 2 * L;
         if (!LP && cold) continue;
 
         f2 o[Q];
@@ -277,21 +256,14 @@ __device__ __forceinline__ void stream2d_row(const StreamArgs &a, const Stream2G
             st.p2[0][b] = slot[0];
             st.p5[0][b] = slot[64];
             st.p6[0][b] = slot[128];
-            if constexpr (UP) {
-                slot[0] = cur[4];
-                slot[64] = shr_kept(cur[7]);
-                slot[128] = shl_kept(cur[8]);
-            } else {
-                slot[0] = cur[2];
-                slot[64] = shl_kept(cur[5]);
-                slot[128] = shr_kept(cur[6]);
-            }
+            slot[0] = cur[2];
+            slot[64] = shl_kept(cur[5]);
+            slot[128] = shr_kept(cur[6]);
             st.c0[b] = cur[0];
             st.c1[b] = shl_kept(cur[1]);
             st.c3[b] = shr_kept(cur[3]);
         }
-        const bool rowlive = UP ? ((!GUARD || y < g.yo1) && (L == S || y >= g.yo0))
-                                : ((!GUARD || y >= g.yo0) && (L == S || y < g.yo1));
+        const bool rowlive = (!GUARD || y >= g.yo0) && (L == S || y < g.yo1);
         if (rowlive) {
             if constexpr (OBST) {
                 const float ua = (oa || !g.owna) ? 0.f : sqrt_av(usq.x);
@@ -371,7 +343,6 @@ __device__ __forceinline__ Stream2Geo stream2d_geo(const StreamArgs &a, int t, i
     g.obp = a.obst_g + (xca + a.og);
     g.j0 = g.yo0 - S;
     g.jlast = g.yo1 + S - 1;
-    g.up = a.mirror && (seg & 1);
     return g;
 }
 
@@ -382,9 +353,10 @@ __device__ __forceinline__ Stream2Geo stream2d_geo(const StreamArgs &a, int t, i
 // parity instead of one register and a copy, which costs 6-8 VGPRs per level
 // (S = 10: 253 VGPRs without spills one row per iteration; 256 + 221 spilled
 // two rows per iteration).
-template <int S, int PD, bool NT, bool OBST, bool TOL, bool LP, bool UP = false>
-__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, const Stream2Geo &g, Stream2State<S> &st,
+template <int S, int PD, bool NT, bool OBST, bool TOL, bool LP>
+__device__ __forceinline__ void stream2d_unit(const StreamArgs &a, int t, int lane, Stream2State<S> &st,
                                               f2 *lpl) {
+    const Stream2Geo g = stream2d_geo<S>(a, t, lane);
     const TolK tk{a.omo, a.tc0, a.tc1, a.tc2};
     if constexpr (LP) {
 #pragma unroll
@@ -401,21 +373,6 @@ __device__ __forceinline__ void stream2d_unit(const StreamArgs &a, const Stream2
     if constexpr (!OBST) {
 #pragma unroll
         for (int b = 0; b < S; ++b) st.tot2[b] = mk2(0.f);
-    }
-    if constexpr (UP) {  // mirrored: rows jlast .. j0
-        stream2d_load<PD, OBST, true>(a, g, g.jlast, st.v[0], st.ob[0]);
-        int j = g.jlast;
-#pragma unroll 1
-        for (int i = 0; i < 2 * S; ++i, --j)
-            stream2d_row<S, 0, true, PD, NT, OBST, TOL, LP, true>(a, g, st, j, tk, lpl);
-#pragma unroll 1
-        for (; j >= g.j0; --j) stream2d_row<S, 0, false, PD, NT, OBST, TOL, LP, true>(a, g, st, j, tk, lpl);
-        if constexpr (!OBST) {
-#pragma unroll
-            for (int b = 0; b < S; ++b)
-                st.tot[b] += (g.owna ? st.tot2[b].x : 0.f) + (g.ownb ? st.tot2[b].y : 0.f);
-        }
-        return;
     }
     stream2d_load<PD, OBST>(a, g, g.j0, st.v[0], st.ob[0]);
     if (PD == 2) stream2d_load<PD, OBST>(a, g, g.j0 + 1, st.v[1], st.ob[1]);
@@ -476,8 +433,7 @@ __device__ __forceinline__ void stream2d_partials(const StreamArgs &a, int idx, 
 // SIMD (AGPRs as spill space, no scratch) S = 7..12 ran 175-214 GLUPS
 // bitwise and 263-314 tolerance against 290 / 333 for S = 6
 // (profiles/r03/ab_lp_depth.log).
-// MIR (LP forms, A/B of LBM_STREAM_MIRROR): odd segments take the mirrored walk.
-template <int S, bool kReduce, int W, bool NT, bool TOL = false, bool LP = false, bool MIR = false>
+template <int S, bool kReduce, int W, bool NT, bool TOL = false, bool LP = false>
 __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
     __shared__ float lds[W];
     __shared__ f2 lds_p[LP ? W * 3 * S * 64 : 1];   // LP: [wave][S][3][64] older rows of planes 2, 5, 6
@@ -501,24 +457,10 @@ __global__ __launch_bounds__(64 * W, 2) void stream_steps2d(StreamArgs a) {
         // per-unit obstacle flag (launch-invariant; scalar load): units that
         // read no obstacle cell run the select-free copy of the unit loop
         typedef const __attribute__((address_space(4))) uint8_t CU8;
-        const Stream2Geo g = stream2d_geo<S>(a, t, lane);
-        const bool ob = a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0;
-        if constexpr (MIR) {
-            if (g.up) {
-                if (ob)
-                    stream2d_unit<S, 1, NT, true, TOL, LP, true>(a, g, st, lpl);
-                else
-                    stream2d_unit<S, 1, NT, false, TOL, LP, true>(a, g, st, lpl);
-            } else if (ob) {
-                stream2d_unit<S, 1, NT, true, TOL, LP>(a, g, st, lpl);
-            } else {
-                stream2d_unit<S, 1, NT, false, TOL, LP>(a, g, st, lpl);
-            }
-        } else if (ob) {
-            stream2d_unit<S, 1, NT, true, TOL, LP>(a, g, st, lpl);
-        } else {
-            stream2d_unit<S, 1, NT, false, TOL, LP>(a, g, st, lpl);
-        }
+        if (a.uobst == nullptr || ((CU8 *)a.uobst)[t] != 0)
+            stream2d_unit<S, 1, NT, true, TOL, LP>(a, t, lane, st, lpl);
+        else
+            stream2d_unit<S, 1, NT, false, TOL, LP>(a, t, lane, st, lpl);
     }
     if (t < max(a.total, 1)) stream2d_partials<S, TOL>(a, t, lane, st);
     if (a.trace && lane == 0 && t < a.total) {
@@ -571,15 +513,6 @@ static void launch_s2d(const StreamArgs &a, int units, bool reduce, hipStream_t 
         hipLaunchKernelGGL((stream_steps2d<S, false, 1, NT, TOL, LP>), dim3(units), dim3(64), 0, s, a);
 }
 
-// the mirrored-walk forms (LBM_STREAM_MIRROR, A/B): tolerance S = 10, bitwise S = 6 (LP)
-template <int S, bool TOL>
-static void launch_s2d_mir(const StreamArgs &a, int units, bool reduce, hipStream_t s) {
-    if (reduce)
-        hipLaunchKernelGGL((stream_steps2d<S, true, 1, false, TOL, true, true>), dim3(units), dim3(64), 0, s, a);
-    else
-        hipLaunchKernelGGL((stream_steps2d<S, false, 1, false, TOL, true, true>), dim3(units), dim3(64), 0, s, a);
-}
-
 template <int S, bool TOL, bool LP>
 static const void *s2d_fn() {
     return (const void *)&stream_steps2d<S, false, 1, false, TOL, LP>;
@@ -626,14 +559,6 @@ hipError_t stream2d_blocks_per_cu(int steps, int cfg, bool tol, int &n) {
 
 hipError_t launch_stream2d(const StreamArgs &a, int units, int steps, bool reduce, int cfg, bool tol, hipStream_t s) {
     if (!s2d_form_ok(steps, cfg, tol)) return hipErrorInvalidValue;
-    if (cfg == 4 && a.mirror && (steps == 10 && tol)) {
-        launch_s2d_mir<10, true>(a, units, reduce, s);
-        return hipGetLastError();
-    }
-    if (cfg == 4 && a.mirror && (steps == 6 && !tol)) {
-        launch_s2d_mir<6, false>(a, units, reduce, s);
-        return hipGetLastError();
-    }
     if (cfg == 4) {
         switch (steps * 2 + (tol ? 1 : 0)) {
             case 12: launch_s2d<6, false, false, true>(a, units, reduce, s); break;

@@ -824,31 +824,3 @@ def test_mid_size_stream_split(gpu_lib, nx, ny):
         e.run_steps(13, accelerate_first=True)
         cells, _ = e.store(n_av=13)
     assert _rel(cells, ref) < TOL_POP
-
-
-# ------------------------------------------------- mirrored walk (A/B) ----
-
-@pytest.mark.parametrize("n,flags,steps", [(8192, 0, 13), (2048, 0, 16), (8192, 4, 23), (2048, 4, 27)])
-def test_mirrored_segment_walk(gpu_lib, n, flags, steps, monkeypatch):
-    """LBM_STREAM_MIRROR=1 (debug knob): odd segments of
-    the LP forms (bitwise S = 6, tolerance S = 10) walk their rows bottom-up
-    with the delay lines of planes 2, 5, 6 and 4, 7, 8 swapped.  Same cells,
-    same arithmetic: the lattice must be bitwise the default walk's (and, in
-    bitwise mode, the oracle's), fused remainders included."""
-    p = lio.Params(n, n, steps, 10, 0.1, 0.005, 1.85)
-    obst = bench_obstacles(n)
-    rng = np.random.default_rng(n + steps)
-    obst[rng.random((n, n)) < 0.002] = 1
-    out = []
-    for mirror in ("0", "1"):
-        monkeypatch.setenv("LBM_STREAM_MIRROR", mirror)
-        with gpu_lib.Engine(p, obst, flags=flags) as e:
-            assert e.kernel_in_use() == "stream" and e.steps_per_launch() == (10 if flags else 6)
-            e.init_equilibrium()
-            e.run_steps(steps, accelerate_first=True)
-            out.append(e.store(n_av=steps))
-    assert np.array_equal(out[0][0], out[1][0])
-    np.testing.assert_allclose(out[1][1], out[0][1], rtol=1e-5)  # |u| partials summed in the other row order
-    if flags == 0 and n <= 2048:
-        ref, _ = oracle.run_mt(p, obst, steps, 16, lio.init_cells(p))
-        assert np.array_equal(out[1][0], ref)
