@@ -29,6 +29,7 @@
 #include <string>
 #include <array>
 #include <vector>
+#include <type_traits>
 
 #include "lbm3d_hip.h"
 #include "lbm_packed.hpp"
@@ -646,8 +647,154 @@ constexpr int T3TH3 = 12;       // rows (waves) per block
 constexpr int T3OY3 = T3TH3 - 6;
 constexpr int GZ3 = 3;  // ghost planes each side of every slab lattice (and obst_g)
 
+// Per-level delay lines of the three-step pass in two register sets used on
+// alternate planes (the plane loop runs two planes per iteration, set P = 0
+// then 1): r0[P ^ 1] / zr[P ^ 1] hold what the previous plane left (speeds 0,
+// 1, 2 of the centre plane; its y +- 1 pulls of speeds 3..8), r0[P] / zr[P]
+// take this plane's; r9[P] holds the speeds 9, 10, 11 of the plane two back
+// and takes this plane's.  (One set per delay line, rotated by copies, cost
+// ~45 moves per plane iteration plus ~40 loop-carried copies at the back edge.)
+struct Lv3 {
+    float r0[2][3], r9[2][3], zr[2][6];
+};
+
+// per-thread LDS offsets (floats) of a level's slots, loop-invariant
+struct Lds3 {
+    int c, ym, yp, ymxm, ypxp, ypxm, ymxp;  // own cell; y-1; y+1; (y-1,x-1); (y+1,x+1); (y+1,x-1); (y-1,x+1)
+};
+
+// level3 for the three-step pass: level L (centre plane jz - 1, input plane
+// jz), register set P as above, for a wave whose row is live for the first D
+// levels (SKIP: D = min(row, 11 - row, 3); every row D = 3 without it).
+// Level L publishes its input only while some live row reads it (L <= D + 1:
+// the rows beside a live row are live one level less) and computes only
+// while live (L <= D); every level meets its barrier.  Liveness is static per
+// instantiation, so no path merges a computed with a skipped result (the
+// merges had cost a register move per population and level).
+// pin / pold: P-ring slots of planes jz and jz - 2 (wave-uniform).
+template <int P, int L, int D, bool TOL>
+__device__ __forceinline__ float level3p(const float (&in)[Q3], float (&out)[Q3], float *lds, int pin, int pold,
+                                         Lv3 &st, const Lds3 &d, bool ob, const Two3Args &a) {
+    constexpr int C = T3<T3TH3>::C;
+    float *M = lds, *Z = lds + 2 * C, *Pr = lds + 8 * C;
+    if constexpr (L <= D + 1) {
+        M[d.c] = in[17];
+        M[C + d.c] = in[18];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Z[i * C + d.c] = in[3 + i];
+        Pr[(pin * 2) * C + d.c] = in[12];
+        Pr[(pin * 2 + 1) * C + d.c] = in[13];
+    }
+    __syncthreads();
+    if constexpr (L > D) {
+        return 0.f;
+    } else {
+        const float *pp = Pr + pold * 2 * C;  // plane jz - 2
+        float s[Q3];
+        s[0] = st.r0[P ^ 1][0];
+        s[1] = dpp_from_left(st.r0[P ^ 1][1]);
+        s[2] = dpp_from_right(st.r0[P ^ 1][2]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) s[3 + i] = st.zr[P ^ 1][i];
+        // plane jz's y +- 1 pulls of speeds 3..8, for the next plane (each
+        // slot is rewritten only after the next barrier of this level)
+        st.zr[P][0] = Z[0 * C + d.ym];
+        st.zr[P][1] = Z[1 * C + d.yp];
+        st.zr[P][2] = Z[2 * C + d.ymxm];
+        st.zr[P][3] = Z[3 * C + d.ypxp];
+        st.zr[P][4] = Z[4 * C + d.ypxm];
+        st.zr[P][5] = Z[5 * C + d.ymxp];
+        s[9] = st.r9[P][0];
+        s[10] = dpp_from_left(st.r9[P][1]);
+        s[11] = dpp_from_right(st.r9[P][2]);
+        s[12] = pp[d.ym];
+        s[13] = pp[C + d.yp];
+        s[14] = in[14];
+        s[15] = dpp_from_right(in[15]);
+        s[16] = dpp_from_left(in[16]);
+        s[17] = M[d.yp];
+        s[18] = M[C + d.ym];
+        float u;
+        if constexpr (TOL)
+            u = cell3dt(s, out, ob, a.omo, a.k0, a.k1, a.k2, a.w1, a.w2);
+        else
+            u = cell3d(s, out, ob, a.omega, a.omo, a.w1, a.w2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            st.r9[P][i] = in[9 + i];
+            st.r0[P][i] = in[i];
+        }
+        return u;
+    }
+}
+
+// The plane loop of one wave (rows live for D levels, see level3p); input
+// planes zs-3 .. ze+2, two per iteration (register sets 0 and 1).  Every
+// plane base and speed offset is wave-uniform: loads and stores are buffer
+// operations on a per-plane descriptor with the speed offset in soffset and
+// the lane's cell in voffset (no per-access 64-bit address arithmetic; the
+// engine keeps Q3 x KS x 4 B below 2^31 for this pass).
+template <int D, bool TOL>
+__device__ __forceinline__ void three_rows(const Two3Args &a, const Lds3 &d, float *lds1, float *lds2, float *lds3,
+                                           int x, int y, unsigned rowb, bool own, int zs, int ze, float &u1,
+                                           float &u2, float &u3) {
+    Lv3 s1{}, s2{}, s3{};
+    const unsigned nrec = (unsigned)(Q3 * a.KS * 4);
+    const int ks4 = (int)(a.KS * 4);
+    auto rsrc = [&](const float *base) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, (int)nrec, 0x00020000);
+    };
+    auto obz = [&](int zz) {  // planes zs-6 .. ze+1 are asked for; only zs-2 .. ze+1 are used
+        zz = min(max(zz, -3), a.nz + 2);
+        return a.obst[((long long)zz * a.ny + y) * a.nx + x] != 0;
+    };
+    float in[Q3];
+    auto load = [&](int pl) {
+        const auto r = rsrc(a.fin + (long long)pl * a.PL);
+#pragma unroll
+        for (int k = 0; k < Q3; ++k) in[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)rowb, k * ks4, 0));
+    };
+    bool ob1 = obz(zs - 4), ob2 = obz(zs - 5), ob3 = obz(zs - 6);
+    load(zs - 3);
+    // P-ring slots (planes mod 3): level L publishes plane j - L + 1 and reads
+    // plane j - L - 1 of input plane j
+    int sj = (((zs - 3) % 3) + 3) % 3;  // slot of plane j
+    auto plane = [&](auto PC, int j) __attribute__((always_inline)) {
+        constexpr int P = decltype(PC)::value;
+        const int sm1 = sj == 0 ? 2 : sj - 1, sm2 = sj == 2 ? 0 : sj + 1;  // slots of j - 1, j - 2 (j - 3: sj)
+        if constexpr (D >= 1) {
+            ob3 = ob2;
+            ob2 = ob1;
+            ob1 = obz(j - 1);
+        }
+        float o1[Q3], o2[Q3], o3[Q3];
+        const float v1 = level3p<P, 1, D, TOL>(in, o1, lds1, sj, sm2, s1, d, ob1, a);
+        if (D == 3 && own && j - 1 >= zs && j - 1 < ze) u1 += v1;
+        load(min(j + 1, ze + 2));
+        const float v2 = level3p<P, 2, D, TOL>(o1, o2, lds2, sm1, sj, s2, d, ob2, a);
+        if (D == 3 && own && j - 2 >= zs && j - 2 < ze) u2 += v2;
+        const float v3 = level3p<P, 3, D, TOL>(o2, o3, lds3, sm2, sm1, s3, d, ob3, a);
+        if constexpr (D == 3) {
+            if (own && j - 3 >= zs && j - 3 < ze) {
+                u3 += v3;
+                const auto r = rsrc(a.fout + (long long)(j - 3) * a.PL);
+#pragma unroll
+                for (int k = 0; k < Q3; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o3[k]), r, (int)rowb, k * ks4, 2);
+            }
+        }
+        sj = sj == 2 ? 0 : sj + 1;
+    };
+    int j = zs - 3;
+    for (; j + 1 <= ze + 2; j += 2) {
+        plane(std::integral_constant<int, 0>{}, j);
+        plane(std::integral_constant<int, 1>{}, j + 1);
+    }
+    if (j <= ze + 2) plane(std::integral_constant<int, 0>{}, j);
+}
+
 // SKIP: rows no later level reads skip the collision (level 1: rows 1..10,
-// level 2: 2..9, level 3: 3..8 live), as step3d_two's SKIP.
+// level 2: 2..9, level 3: 3..8 live), as step3d_two's SKIP -- each wave runs
+// the plane loop instantiated for its row's live depth.
 template <bool TOL, bool SKIP>
 __global__ __launch_bounds__(T3W *T3TH3) void step3d_three(Two3Args a) {
     __shared__ float lds1[T3<T3TH3>::LDS], lds2[T3<T3TH3>::LDS], lds3[T3<T3TH3>::LDS];
@@ -660,49 +807,26 @@ __global__ __launch_bounds__(T3W *T3TH3) void step3d_three(Two3Args a) {
     const bool own = lane >= 3 && lane < T3W - 3 && wy >= 3 && wy < T3TH3 - 3 && ox + lane - 3 < a.nx &&
                      oy + wy - 3 < a.ny;
     const int zs = a.z0 + B.z * a.seg, ze = min(zs + a.seg, a.zn);
-    const long long row = (long long)y * a.px + x;
-    float r0a[3] = {0.f, 0.f, 0.f}, r9aa[3] = {0.f, 0.f, 0.f}, r9ba[3] = {0.f, 0.f, 0.f};
-    float r0b[3] = {0.f, 0.f, 0.f}, r9ab[3] = {0.f, 0.f, 0.f}, r9bb[3] = {0.f, 0.f, 0.f};
-    float r0c[3] = {0.f, 0.f, 0.f}, r9ac[3] = {0.f, 0.f, 0.f}, r9bc[3] = {0.f, 0.f, 0.f};
-    float zra[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, zrb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float zrc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float u1 = 0.f, u2 = 0.f, u3 = 0.f;
-    auto obz = [&](int zz) {  // planes zs-6 .. ze+1 are asked for; only zs-2 .. ze+1 are used
-        zz = min(max(zz, -3), a.nz + 2);
-        return a.obst[((long long)zz * a.ny + y) * a.nx + x] != 0;
-    };
-    float in[Q3];
-    bool ob1 = obz(zs - 4), ob2 = obz(zs - 5), ob3 = obz(zs - 6);
+    const unsigned rowb = (unsigned)(y * a.px + x) * 4u;  // byte offset of the lane's cell in a speed plane
+    Lds3 d;
     {
-        const float *pl = a.fin + (long long)(zs - 3) * a.PL + row;
-#pragma unroll
-        for (int k = 0; k < Q3; ++k) in[k] = pl[k * a.KS];
+        const int wm = max(wy - 1, 0) * T3W, wp = min(wy + 1, T3TH3 - 1) * T3W;
+        const int lm = max(lane - 1, 0), lp = min(lane + 1, T3W - 1);
+        d.c = wy * T3W + lane;
+        d.ym = wm + lane;
+        d.yp = wp + lane;
+        d.ymxm = wm + lm;
+        d.ypxp = wp + lp;
+        d.ypxm = wp + lm;
+        d.ymxp = wm + lp;
     }
-    for (int j = zs - 3; j <= ze + 2; ++j) {
-        const float *pn = a.fin + (long long)min(j + 1, ze + 2) * a.PL + row;
-        ob3 = ob2;
-        ob2 = ob1;
-        ob1 = obz(j - 1);
-        float o1[Q3], o2[Q3], o3[Q3];
-        constexpr int R = T3TH3;
-        const float v1 = level3<T3TH3, TOL>(in, o1, lds1, j, r0a, r9aa, r9ba, zra, lane, wy, ob1,
-                                            !SKIP || (wy >= 1 && wy < R - 1), a);
-        if (own && j - 1 >= zs && j - 1 < ze) u1 += v1;
-        // level 1 is done with plane j: its registers take plane j + 1, in
-        // flight across levels 2 and 3
-#pragma unroll
-        for (int k = 0; k < Q3; ++k) in[k] = pn[k * a.KS];
-        const float v2 = level3<T3TH3, TOL>(o1, o2, lds2, j - 1, r0b, r9ab, r9bb, zrb, lane, wy, ob2,
-                                            !SKIP || (wy >= 2 && wy < R - 2), a);
-        if (own && j - 2 >= zs && j - 2 < ze) u2 += v2;
-        const float v3 = level3<T3TH3, TOL>(o2, o3, lds3, j - 2, r0c, r9ac, r9bc, zrc, lane, wy, ob3,
-                                            !SKIP || (wy >= 3 && wy < R - 3), a);
-        if (own && j - 3 >= zs && j - 3 < ze) {
-            u3 += v3;
-            float *d = a.fout + (long long)(j - 3) * a.PL + row;
-#pragma unroll
-            for (int k = 0; k < Q3; ++k) __builtin_nontemporal_store(o3[k], d + k * a.KS);
-        }
+    float u1 = 0.f, u2 = 0.f, u3 = 0.f;
+    const int depth = SKIP ? min(min(wy, T3TH3 - 1 - wy), 3) : 3;  // wave-uniform
+    switch (depth) {
+        case 0: three_rows<0, TOL>(a, d, lds1, lds2, lds3, x, y, rowb, own, zs, ze, u1, u2, u3); break;
+        case 1: three_rows<1, TOL>(a, d, lds1, lds2, lds3, x, y, rowb, own, zs, ze, u1, u2, u3); break;
+        case 2: three_rows<2, TOL>(a, d, lds1, lds2, lds3, x, y, rowb, own, zs, ze, u1, u2, u3); break;
+        default: three_rows<3, TOL>(a, d, lds1, lds2, lds3, x, y, rowb, own, zs, ze, u1, u2, u3); break;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1261,6 +1385,8 @@ struct lbm3d_handle {
     // 3 planes of the neighbours, exchanged once per pass)
     bool use_three() const {
         if (three == 0 || !use_two()) return false;
+        // step3d_three addresses a plane's speeds by 32-bit buffer offsets
+        if ((long long)Q3 * KS * 4 >= (1LL << 31)) return false;
         if (!multi()) return true;
         for (int n : all_nz)
             if (n < 6) return false;
