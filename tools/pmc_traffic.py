@@ -61,12 +61,18 @@ def main():
     ap.add_argument("--sq", default=None, help="SQ pass csv (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE)")
     ap.add_argument("--simds", type=int, default=1024, help="SIMDs of the device (256 CUs x 4)")
     ap.add_argument("--profile", default=None, help="where the csv files are committed (recorded in the entry)")
+    ap.add_argument("--bytes-per-cell", type=float, default=72.0,
+                    help="algorithmic bytes per cell and launch (72: D2Q9; 152: a D3Q19 pass)")
+    ap.add_argument("--fetch-mult", type=float, default=2.0,
+                    help="FETCH_SIZE multiplier: 2 for 16 B/lane streams (guide); otherwise calibrated "
+                         "on a kernel of the same access width with a known byte count (--fetch-note)")
+    ap.add_argument("--fetch-note", default="gfx950 wide-stream undercount")
     a = ap.parse_args()
     fetch_kib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
     write_kib, nw = per_launch(a.write, "WRITE_SIZE", a.kernel)
-    read_b = 2.0 * fetch_kib * 1024
+    read_b = a.fetch_mult * fetch_kib * 1024
     write_b = write_kib * 1024
-    alg = 72 * a.cells
+    alg = a.bytes_per_cell * a.cells
     entry = {
         "kernel": a.kernel, "launches_fetch": nf, "launches_write": nw,
         "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
@@ -74,7 +80,7 @@ def main():
         "hbm_bytes_per_launch": read_b + write_b,
         "algorithmic_bytes_per_launch": alg,
         "ratio_to_algorithmic": round((read_b + write_b) / alg, 4),
-        "correction": "FETCH_SIZE x2 (gfx950 wide-stream undercount), KiB x1024",
+        "correction": f"FETCH_SIZE x{a.fetch_mult:g} ({a.fetch_note}), KiB x1024",
     }
     if a.sq:
         sq, nd = per_dispatch(a.sq, a.kernel)
