@@ -483,7 +483,7 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
     comp_b = (n3 * 152 / 3 + n2 * 152 / 2 + (steps - n3 - n2) * 152) / max(steps, 1)
     per_gpu_gbs = alg_b * cells / world * steps / dev / 1e9
     comp_gbs = comp_b * cells / world * steps / dev / 1e9
-    return {"grid": f"{n}^3", "steps": steps, "settle_steps": nset, "decomposition": f"{world} z slabs",
+    res = {"grid": f"{n}^3", "steps": steps, "settle_steps": nset, "decomposition": f"{world} z slabs",
             "numerics": "tolerance" if flags & native.FLAG_TOLERANCE else "bitwise",
             "kernel": (f"step3d_three ({n3 // 3} passes of 3 steps) + step3d_two ({n2 // 2} of 2)" if three else
                        "step3d_two (2 steps per pass)" if two else "step3d_pair (1 step per launch)"),
@@ -497,6 +497,16 @@ def aux_d3q19(n: int, steps: int, rank: int, world: int, local_rank: int, dist_o
             "note": f"hbm_frac: {alg_b:.1f} B per update including the blocks' overlap re-reads; hbm_frac_compulsory: "
                     f"{comp_b:.1f} B per update, the lattice once per pass (152 B = 19 fp32 loads + stores per cell; "
                     "effective_gbs on that basis per step); parity unpinned upstream (no 3-D reference)"}
+    # the committed PMC passes of this pass on one GPU (tools/pmc_traffic.py,
+    # profiles/traffic.json): HBM bytes per three-step pass against the
+    # compulsory 152 B x cells, the VALU pipe's busy fraction
+    prof = load_traffic(f"{n}^3/three{'t' if flags & native.FLAG_TOLERANCE else 'b'}") if world == 1 and three else {}
+    if prof:
+        res["pmc"] = {"hbm_bytes_per_pass": prof.get("hbm_bytes_per_launch"),
+                      "ratio_to_compulsory": prof.get("ratio_to_algorithmic"),
+                      "valu_busy": (prof.get("valu") or {}).get("busy_frac"),
+                      "correction": prof.get("correction"), "profile": prof.get("profile")}
+    return res
 
 
 def _check_cases(world: int):
