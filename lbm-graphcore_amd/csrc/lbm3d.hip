@@ -779,7 +779,12 @@ __device__ __forceinline__ void three_rows(const Two3Args &a, const Lds3 &d, flo
                 u3 += v3;
                 const auto r = rsrc(a.fout + (long long)(j - 3) * a.PL);
 #pragma unroll
-                for (int k = 0; k < Q3; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o3[k]), r, (int)rowb, k * ks4, 2);
+                // plain (temporal) stores: x-neighbouring blocks run on one XCD
+                // and each writes a 232-B unaligned row segment, which the L2
+                // merges into whole lines before they leave (non-temporal
+                // stores: 2.11-2.30 vs 2.07 ms per step at 512^3 tolerance,
+                // profiles/r06/d3store/)
+                for (int k = 0; k < Q3; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o3[k]), r, (int)rowb, k * ks4, 0);
             }
         }
         sj = sj == 2 ? 0 : sj + 1;
